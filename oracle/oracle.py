@@ -1,0 +1,165 @@
+"""ctypes wrapper for oracle/libgp_oracle.so (the CPU restatement).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, always as the checker or the timed CPU baseline — never as the product.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgp_oracle.so")
+
+TOPOLOGIES = {"line": 0, "full": 1, "2D": 2, "Imp3D": 3, "3D": 4}
+ALGOS = {"gossip": 0, "push-sum": 1}
+
+
+class Config(C.Structure):
+    _fields_ = [("n_arg", C.c_int64), ("topology", C.c_int32), ("algo", C.c_int32),
+                ("seed", C.c_uint64), ("delta", C.c_double), ("gossip_threshold", C.c_int32),
+                ("term_init", C.c_int32), ("term_limit", C.c_int32)]
+
+
+class Layout(C.Structure):
+    _fields_ = [("nodes", C.c_int64), ("actors", C.c_int64), ("grid", C.c_int64),
+                ("leader", C.c_int64), ("participants", C.c_int64)]
+
+
+class Status(C.Structure):
+    _fields_ = [("round", C.c_int64), ("completed", C.c_int64), ("converged", C.c_int32),
+                ("pad", C.c_int32), ("sum_s", C.c_double), ("sum_w", C.c_double)]
+
+
+_lib = None
+
+
+def build():
+    """Compile the oracle with its Makefile (gcc, no GPU needed)."""
+    import subprocess
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        L.gpo_create.restype = P
+        L.gpo_create.argtypes = [C.POINTER(Config), C.POINTER(Layout)]
+        L.gpo_step.argtypes = [P, C.c_int64, C.c_int32, C.POINTER(Status)]
+        L.gpo_degree.argtypes = [P, C.c_int64]
+        L.gpo_neighbors.argtypes = [P, C.c_int64, P, C.c_int32]
+        L.gpo_read_gossip.argtypes = [P, C.c_int64, C.c_int64, P, P]
+        L.gpo_read_pushsum.argtypes = [P, C.c_int64, C.c_int64, P, P, P]
+        L.gpo_read_messages.argtypes = [P, C.c_int64, C.c_int64, P, P, P]
+        L.gpo_read_trace.argtypes = [P, C.c_int64, C.c_int64, P]
+        L.gpo_destroy.argtypes = [P]
+        L.gpo_sizes.argtypes = [C.c_int64, C.c_int32, P, P, P]
+        L.gpo_philox4x32_10.argtypes = [P, P, P]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def philox(ctr, key):
+    c = np.asarray(ctr, np.uint32)
+    k = np.asarray(key, np.uint32)
+    out = np.zeros(4, np.uint32)
+    lib().gpo_philox4x32_10(_ptr(c), _ptr(k), _ptr(out))
+    return out
+
+
+def sizes(n_arg, topology):
+    t = TOPOLOGIES[topology] if isinstance(topology, str) else topology
+    v = np.zeros(3, np.int64)
+    rc = lib().gpo_sizes(n_arg, t, _ptr(v[0:1]), _ptr(v[1:2]), _ptr(v[2:3]))
+    if rc:
+        raise ValueError(f"invalid size {n_arg} {topology}")
+    return int(v[0]), int(v[1]), int(v[2])
+
+
+class OracleSim:
+    """One simulation in the CPU restatement; mirrors the product's Simulator API."""
+
+    def __init__(self, n_arg, topology, algo, seed=1, delta=1e-10, gossip_threshold=10,
+                 term_init=1, term_limit=3):
+        t = TOPOLOGIES[topology] if isinstance(topology, str) else topology
+        a = ALGOS[algo] if isinstance(algo, str) else algo
+        self.cfg = Config(n_arg, t, a, seed, delta, gossip_threshold, term_init, term_limit)
+        self.layout = Layout()
+        self.algo = a
+        h = lib().gpo_create(C.byref(self.cfg), C.byref(self.layout))
+        if not h:
+            raise ValueError(f"gpo_create failed for {n_arg} {topology} {algo}")
+        self.h = C.c_void_p(h)
+        self.status = Status()
+
+    @property
+    def actors(self):
+        return int(self.layout.actors)
+
+    def step(self, max_rounds=1 << 40, threads=0):
+        rc = lib().gpo_step(self.h, max_rounds, threads, C.byref(self.status))
+        if rc:
+            raise RuntimeError(f"gpo_step rc={rc}")
+        return self.status
+
+    def degree(self, v):
+        return lib().gpo_degree(self.h, v)
+
+    def neighbors(self, v):
+        out = np.zeros(max(1, self.degree(v)), np.uint32)
+        d = lib().gpo_neighbors(self.h, v, _ptr(out), len(out))
+        return out[:d]
+
+    def read_gossip(self):
+        n = self.actors
+        cnt = np.zeros(n, np.uint32)
+        flags = np.zeros(n, np.uint8)
+        if lib().gpo_read_gossip(self.h, 0, n, _ptr(cnt), _ptr(flags)):
+            raise RuntimeError("read_gossip")
+        return cnt, flags
+
+    def read_pushsum(self):
+        n = self.actors
+        S = np.zeros(n, np.float64)
+        W = np.zeros(n, np.float64)
+        flags = np.zeros(n, np.uint8)
+        if lib().gpo_read_pushsum(self.h, 0, n, _ptr(S), _ptr(W), _ptr(flags)):
+            raise RuntimeError("read_pushsum")
+        return S, W, flags
+
+    def read_messages(self):
+        n = self.actors
+        d = np.zeros(n, np.uint32)
+        s = np.zeros(n, np.float64)
+        w = np.zeros(n, np.float64)
+        if lib().gpo_read_messages(self.h, 0, n, _ptr(d), _ptr(s), _ptr(w)):
+            raise RuntimeError("read_messages")
+        return d, s, w
+
+    def read_trace(self):
+        r = int(self.status.round)
+        out = np.zeros(r, np.int64)
+        if r and lib().gpo_read_trace(self.h, 0, r, _ptr(out)):
+            raise RuntimeError("read_trace")
+        return out
+
+    def close(self):
+        if self.h:
+            lib().gpo_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
