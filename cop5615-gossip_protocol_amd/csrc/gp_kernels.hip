@@ -1,0 +1,584 @@
+// gp_kernels.hip — gfx950 kernels of the synchronous-round gossip / push-sum engine.
+//
+// Every round kernel F(r) is one HBM-streaming pass over the actors:
+//   * collect: the messages sent to actor v in round r-1 are PULLED from v's in-neighbours —
+//     implicit grid offsets (program.fs:295-306 is symmetric) plus the ascending CSR of Imp3D
+//     extra-link sources — in ascending source order, so the fp64 inbox sum is the canonical
+//     sequential one with no sort and no atomics;
+//   * update: program.fs:97-105 (gossip) / :119-143 (push-sum) for one round;
+//   * emit:   one Philox4x32-10 block per (actor, round) picks the neighbour index(es);
+//             only a 1-byte direction code (+ the 16-byte (s,w) message) is stored;
+//   * count:  newly reported actors are reduced per wave/block and added once per block to
+//             total[r], the per-round ParentActor count (program.fs:44-63).
+// Kernels are grid-stride over an XCD-aware node mapping: workgroups with equal blockIdx % 8
+// (one XCD under round-robin dispatch) walk one contiguous 1/8 of the actors, so the +-1,
+// +-G and +-G^2 neighbour rows they re-read stay in that XCD's L2 (placement is a speed hint
+// only; correctness never depends on it).
+#include "gp_kernels.h"
+
+namespace gp {
+
+namespace {
+
+__device__ __forceinline__ void node_range(uint32_t n, uint32_t span, uint32_t& v, uint32_t& end,
+                                           uint32_t& step) {
+    const uint32_t grp = blockIdx.x & 7u;
+    const uint32_t j = blockIdx.x >> 3;
+    const uint32_t per = gridDim.x >> 3;
+    const uint32_t base = grp * span;
+    end = base + span < n ? base + span : n;
+    if (base >= n) end = 0;
+    v = base + j * kBlock + threadIdx.x;
+    step = per * kBlock;
+}
+
+// Block-wide sum of one u32 per thread; thread 0 adds it to *dst when nonzero.
+__device__ __forceinline__ void block_add(uint32_t c, unsigned long long* dst) {
+    __shared__ uint32_t red[kBlock / 64];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int i = 0; i < kBlock / 64; ++i) t += red[i];
+        if (t) atomicAdd(dst, (unsigned long long)t);
+    }
+}
+
+// Push-sum skip gate.  total[r-1] is final (written by earlier launches), so every block takes
+// the same branch; block 0 seeds total[r] with it so the count stays cumulative even when the
+// round is skipped after convergence.
+__device__ __forceinline__ bool ps_gate(const RoundArgs& a) {
+    const unsigned long long prev = a.r ? a.total[a.r - 1] : 0ull;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&a.total[a.r], prev);
+    return prev >= a.target;
+}
+
+// Gossip skip gate: F(r) applies round r-1, so it seeds total[r-1] with total[r-2].
+__device__ __forceinline__ bool gs_gate(const RoundArgs& a) {
+    const unsigned long long prev = a.r >= 2 ? a.total[a.r - 2] : 0ull;
+    if (a.r >= 1 && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&a.total[a.r - 1], prev);
+    return prev >= a.target;
+}
+
+// program.fs:119-143 for one actor (round 0 = :110-116): absorb, test, halve, emit.
+// Returns the new message (s,w); sets conv_now when the actor converges this round.
+struct PsOut {
+    double2 msg;
+    bool send;
+    bool conv_now;
+};
+
+__device__ __forceinline__ PsOut ps_update(uint8_t& f, double2 held, double ss, double ww, uint32_t cin,
+                                           double delta, uint32_t term_limit) {
+    PsOut o;
+    o.conv_now = false;
+    if (f & 16u) {  // alreadyConverged: relay what arrived, if anything (program.fs:125-127)
+        o.send = cin > 0;
+        o.msg = make_double2(ss, ww);
+        return o;
+    }
+    const double S = held.x, W = held.y;
+    const double nS = S + ss, nW = W + ww;  // program.fs:120-121
+    uint32_t term = f & 15u;
+    if (cin > 0) {
+        const double cal = fabs(S / W - nS / nW);  // program.fs:123
+        term = cal > delta ? 0u : term + 1u;       // program.fs:130-133
+        if (term == term_limit) {                  // program.fs:135-138
+            term = 0u;
+            o.conv_now = true;
+        }
+    }
+    f = (uint8_t)(term | (o.conv_now ? 16u : 0u));
+    o.msg = make_double2(nS * 0.5, nW * 0.5);  // program.fs:140-141 (x/2 == x*0.5 exactly)
+    o.send = true;
+    return o;
+}
+
+// ------------------------------------------------------------------ push-sum, grid topologies
+template <bool LINK>
+__global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
+    if (ps_gate(a)) return;
+    const Geom g = a.g;
+    const uint32_t r = a.r;
+    uint32_t v, end, step;
+    node_range(g.actors, a.span, v, end, step);
+    uint32_t newly = 0;
+    for (; v < end; v += step) {
+        const uint32_t m = presence(g, v);
+        if (!m) continue;  // non-participant: never sends, never receives
+        uint8_t f = a.flags[v];
+        double ss = 0.0, ww = 0.0;  // inbox sum from +0.0 in ascending source order
+        uint32_t cin = 0;
+        if (r) {
+            // directions of the in-neighbours' round r-1 messages (6 independent byte loads)
+            const uint8_t dzm = (m & 16u) ? a.dir_prev[v - g.plane] : kDirNone;
+            const uint8_t dym = (m & 4u) ? a.dir_prev[v - g.gx] : kDirNone;
+            const uint8_t dxm = (m & 1u) ? a.dir_prev[v - 1u] : kDirNone;
+            const uint8_t dxp = (m & 2u) ? a.dir_prev[v + 1u] : kDirNone;
+            const uint8_t dyp = (m & 8u) ? a.dir_prev[v + g.gx] : kDirNone;
+            const uint8_t dzp = (m & 32u) ? a.dir_prev[v + g.plane] : kDirNone;
+            uint32_t li = 0, le = 0;
+            if (LINK) {
+                li = a.rev_off[v];
+                le = a.rev_off[v + 1];
+            }
+            auto take = [&](uint32_t u) {
+                const double2 mm = a.msg_prev[u];
+                ss += mm.x;
+                ww += mm.y;
+                ++cin;
+            };
+            // link sources below `bound`, in ascending order (duplicates of a grid neighbour
+            // are harmless: a sender's single code matches at most one of the two entries)
+            auto flush = [&](uint32_t bound) {
+                if (LINK) {
+                    while (li < le) {
+                        const uint32_t s = a.rev_src[li];
+                        if (s >= bound) break;
+                        if (a.dir_prev[s] == kDirLink) take(s);
+                        ++li;
+                    }
+                }
+            };
+            if (m & 16u) { flush(v - g.plane); if (dzm == 5) take(v - g.plane); }
+            if (m & 4u) { flush(v - g.gx); if (dym == 3) take(v - g.gx); }
+            if (m & 1u) { flush(v - 1u); if (dxm == 1) take(v - 1u); }
+            if (m & 2u) { flush(v + 1u); if (dxp == 0) take(v + 1u); }
+            if (m & 8u) { flush(v + g.gx); if (dyp == 2) take(v + g.gx); }
+            if (m & 32u) { flush(v + g.plane); if (dzp == 4) take(v + g.plane); }
+            flush(0xFFFFFFFFu);
+        }
+        double2 held;
+        if (!(f & 16u)) held = r ? a.msg_prev[v] : make_double2((double)v, 1.0);  // InitializeVariables
+        const uint8_t f0 = f;
+        const PsOut o = ps_update(f, held, ss, ww, cin, a.delta, a.term_limit);
+        uint8_t code = kDirNone;
+        if (o.send) {
+            const uint4 x = philox(v, r, kStreamPush, a.seed);
+            code = (uint8_t)kth_bit(m, scale_draw(x.x, popc(m)));
+            a.msg_cur[v] = o.msg;
+        }
+        a.dir_cur[v] = code;
+        if (f != f0) a.flags[v] = f;
+        if (o.conv_now) {
+            a.frozen[v] = o.msg;
+            ++newly;
+        }
+    }
+    block_add(newly, &a.total[r]);
+}
+
+// ------------------------------------------------------------------ gossip, grid topologies
+__device__ __forceinline__ uint32_t nib_match(uint8_t b, uint32_t code) {
+    return (uint32_t)((b & 15u) == code) + (uint32_t)((b >> 4) == code);
+}
+
+template <bool LINK>
+__global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
+    if (gs_gate(a)) return;
+    const Geom g = a.g;
+    const uint32_t r = a.r;
+    uint32_t v, end, step;
+    node_range(g.actors, a.span, v, end, step);
+    uint32_t newly = 0;
+    for (; v < end; v += step) {
+        const uint32_t m = presence(g, v);
+        if (!m) continue;
+        const uint8_t st = a.gstate[v];
+        uint32_t tok = st & 3u;
+        uint32_t done = (st >> 2) & 1u;
+        if (r && !done) {  // apply round r-1: receipts while not done at round start (program.fs:92)
+            uint32_t inc = 0;
+            if (m & 16u) inc += nib_match(a.dir_prev[v - g.plane], 5);
+            if (m & 4u) inc += nib_match(a.dir_prev[v - g.gx], 3);
+            if (m & 1u) inc += nib_match(a.dir_prev[v - 1u], 1);
+            if (m & 2u) inc += nib_match(a.dir_prev[v + 1u], 0);
+            if (m & 8u) inc += nib_match(a.dir_prev[v + g.gx], 2);
+            if (m & 32u) inc += nib_match(a.dir_prev[v + g.plane], 4);
+            if (LINK) {
+                const uint32_t le = a.rev_off[v + 1];
+                for (uint32_t li = a.rev_off[v]; li < le; ++li) inc += nib_match(a.dir_prev[a.rev_src[li]], kDirLink);
+            }
+            if (inc) {
+                const uint32_t c0 = a.cnt[v], c1 = c0 + inc;
+                a.cnt[v] = c1;
+                if (c0 == 0) ++tok;                                  // program.fs:99-100
+                if (c0 <= a.threshold && c1 > a.threshold) {         // program.fs:102-104
+                    done = 1;
+                    ++newly;
+                }
+                a.gstate[v] = (uint8_t)(tok | (done << 2));
+            }
+        }
+        if (tok) {  // emit round r: one draw per activation chain (program.fs:89-95)
+            const uint4 x = philox(v, r, kStreamGossip, a.seed);
+            const uint32_t d = popc(m);
+            const uint32_t c0 = kth_bit(m, scale_draw(x.x, d));
+            const uint32_t c1 = tok > 1 ? kth_bit(m, scale_draw(x.y, d)) : 15u;
+            a.dir_cur[v] = (uint8_t)(c0 | (c1 << 4));
+        }
+    }
+    if (r) block_add(newly, &a.total[r - 1]);
+}
+
+// ------------------------------------------------------------------ generic (bucketed) paths
+__device__ __forceinline__ uint32_t generic_deg(const RoundArgs& a, uint32_t v, uint32_t& m) {
+    if (a.full) {
+        m = 0;
+        return a.nodes;  // all j != v among 0..nodes (program.fs:201-206)
+    }
+    m = presence(a.g, v);
+    return popc(m);
+}
+
+__device__ __forceinline__ uint32_t generic_target(const RoundArgs& a, uint32_t v, uint32_t m, uint32_t idx) {
+    if (a.full) return idx + (idx >= v ? 1u : 0u);
+    const uint32_t code = kth_bit(m, idx);
+    return dir_target(a.g, v, code, code == kDirLink ? a.link[v] : 0u);
+}
+
+// Gossip on any topology (used for "full"): receipts are integer atomics into inc_cur[t]
+// (order-free, so exact); the done filter of program.fs:92 is applied receiver-side.
+__global__ __launch_bounds__(kBlock) void k_gs_push(RoundArgs a) {
+    if (gs_gate(a)) return;
+    const uint32_t r = a.r;
+    uint32_t v, end, step;
+    node_range(a.g.actors, a.span, v, end, step);
+    uint32_t newly = 0;
+    for (; v < end; v += step) {
+        uint32_t m;
+        const uint32_t d = generic_deg(a, v, m);
+        if (!d) continue;
+        const uint8_t st = a.gstate[v];
+        uint32_t tok = st & 3u;
+        uint32_t done = (st >> 2) & 1u;
+        if (r) {
+            const uint32_t inc = a.inc_prev[v];
+            if (inc) {
+                a.inc_prev[v] = 0;
+                if (!done) {
+                    const uint32_t c0 = a.cnt[v], c1 = c0 + inc;
+                    a.cnt[v] = c1;
+                    if (c0 == 0) ++tok;
+                    if (c0 <= a.threshold && c1 > a.threshold) {
+                        done = 1;
+                        ++newly;
+                    }
+                    a.gstate[v] = (uint8_t)(tok | (done << 2));
+                }
+            }
+        }
+        if (tok) {
+            const uint4 x = philox(v, r, kStreamGossip, a.seed);
+            atomicAdd(&a.inc_cur[generic_target(a, v, m, scale_draw(x.x, d))], 1u);
+            if (tok > 1) atomicAdd(&a.inc_cur[generic_target(a, v, m, scale_draw(x.y, d))], 1u);
+        }
+    }
+    if (r) block_add(newly, &a.total[r - 1]);
+}
+
+// Push-sum on any topology (used for "full"): messages are bucketed by destination with an
+// integer atomic (slot order is arbitrary), then each receiver visits its bucket in ascending
+// source order (selection by repeated minimum; buckets hold ~1 entry), so the fp64 sum is the
+// canonical one.
+__global__ __launch_bounds__(kBlock) void k_ps_push_emit(RoundArgs a) {
+    if (ps_gate(a)) return;
+    const uint32_t r = a.r;
+    uint32_t v, end, step;
+    node_range(a.g.actors, a.span, v, end, step);
+    uint32_t newly = 0;
+    for (; v < end; v += step) {
+        uint32_t m;
+        const uint32_t d = generic_deg(a, v, m);
+        if (!d) continue;
+        uint8_t f = a.flags[v];
+        double ss = 0.0, ww = 0.0;
+        uint32_t cin = 0;
+        if (r) {
+            const uint32_t n = a.bcnt_prev[v];
+            if (n) {
+                const uint32_t o = a.boff_prev[v];
+                long long last = -1;
+                for (uint32_t i = 0; i < n; ++i) {
+                    uint32_t best = 0xFFFFFFFFu;
+                    for (uint32_t j = 0; j < n; ++j) {
+                        const uint32_t s = a.slot_prev[o + j];
+                        if ((long long)s > last && s < best) best = s;
+                    }
+                    const double2 mm = a.msg_prev[best];
+                    ss += mm.x;
+                    ww += mm.y;
+                    last = best;
+                }
+                cin = n;
+                a.bcnt_prev[v] = 0;  // bucket consumed; buffer is reused two rounds later
+            }
+        }
+        double2 held;
+        if (!(f & 16u)) held = r ? a.msg_prev[v] : make_double2((double)v, 1.0);
+        const uint8_t f0 = f;
+        const PsOut o = ps_update(f, held, ss, ww, cin, a.delta, a.term_limit);
+        uint32_t t = 0xFFFFFFFFu;
+        if (o.send) {
+            const uint4 x = philox(v, r, kStreamPush, a.seed);
+            t = generic_target(a, v, m, scale_draw(x.x, d));
+            a.msg_cur[v] = o.msg;
+            a.pos_cur[v] = atomicAdd(&a.bcnt_cur[t], 1u);
+        }
+        a.tgt_cur[v] = t;
+        if (f != f0) a.flags[v] = f;
+        if (o.conv_now) {
+            a.frozen[v] = o.msg;
+            ++newly;
+        }
+    }
+    block_add(newly, &a.total[r]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_ps_push_fill(RoundArgs a, uint32_t* slot_cur, const uint32_t* boff_cur) {
+    const unsigned long long prev = a.r ? a.total[a.r - 1] : 0ull;
+    if (prev >= a.target) return;
+    uint32_t v, end, step;
+    node_range(a.g.actors, a.span, v, end, step);
+    for (; v < end; v += step) {
+        const uint32_t t = a.tgt_cur[v];
+        if (t != 0xFFFFFFFFu) slot_cur[boff_cur[t] + a.pos_cur[v]] = v;
+    }
+}
+
+// ------------------------------------------------------------------ setup / utility kernels
+__global__ void k_links(uint32_t* link, uint32_t nodes, uint64_t seed) {
+    // program.fs:309: Random().Next(0, nodes-1) -> [0, nodes-2]
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < nodes; v += gridDim.x * blockDim.x)
+        link[v] = scale_draw(philox(v, 0u, kStreamTopo, seed).x, nodes - 1u);
+}
+
+__global__ void k_count(const uint32_t* idx, uint32_t n, uint32_t* counts) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        atomicAdd(&counts[idx[i]], 1u);
+}
+
+__global__ void k_rev_fill(const uint32_t* link, uint32_t nodes, const uint32_t* rev_off, uint32_t* fillc,
+                           uint32_t* rev_src) {
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < nodes; v += gridDim.x * blockDim.x) {
+        const uint32_t t = link[v];
+        rev_src[rev_off[t] + atomicAdd(&fillc[t], 1u)] = v;
+    }
+}
+
+__global__ void k_sort_segments(const uint32_t* off, uint32_t* vals, uint32_t n) {
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
+        const uint32_t b = off[v], e = off[v + 1];
+        for (uint32_t i = b + 1; i < e; ++i) {  // insertion sort; segments are short
+            const uint32_t x = vals[i];
+            uint32_t j = i;
+            while (j > b && vals[j - 1] > x) {
+                vals[j] = vals[j - 1];
+                --j;
+            }
+            vals[j] = x;
+        }
+    }
+}
+
+constexpr uint32_t kScanPer = 8;
+constexpr uint32_t kScanTile = kBlock * kScanPer;
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t& total) {
+    __shared__ uint32_t wsum[kBlock / 64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off, 64);
+        if (lane >= (uint32_t)off) inc += y;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+    total = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kBlock / 64; ++i) {
+        if (i < w) base += wsum[i];
+        total += wsum[i];
+    }
+    __syncthreads();
+    return base + inc - x;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* in, uint32_t n, uint32_t* sums) {
+    const uint32_t b0 = blockIdx.x * kScanTile;
+    uint32_t s = 0;
+    for (uint32_t i = threadIdx.x; i < kScanTile; i += kBlock) {
+        const uint32_t k = b0 + i;
+        if (k < n) s += in[k];
+    }
+    uint32_t total;
+    block_excl_scan(s, total);
+    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_top(uint32_t* sums, uint32_t nb) {
+    uint32_t carry = 0;
+    for (uint32_t b = 0; b < nb; b += kBlock) {
+        const uint32_t i = b + threadIdx.x;
+        const uint32_t x = i < nb ? sums[i] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_excl_scan(x, total);
+        if (i < nb) sums[i] = carry + ex;
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_apply(const uint32_t* in, uint32_t* off, uint32_t n,
+                                                        const uint32_t* sums) {
+    const uint32_t b0 = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    uint32_t vals[kScanPer];
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kScanPer; ++j) {
+        const uint32_t k = b0 + j;
+        vals[j] = k < n ? in[k] : 0u;
+        s += vals[j];
+    }
+    uint32_t total;
+    uint32_t run = sums[blockIdx.x] + block_excl_scan(s, total);
+#pragma unroll
+    for (uint32_t j = 0; j < kScanPer; ++j) {
+        const uint32_t k = b0 + j;
+        if (k < n) off[k] = run;
+        run += vals[j];
+        if (k + 1 == n) off[n] = run;
+    }
+}
+
+__global__ void k_fill_u8(uint8_t* p, uint8_t val, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        p[i] = val;
+}
+
+__global__ void k_ps_init(uint8_t* flags, Geom g, uint32_t full, uint32_t term_init) {
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < g.actors; v += gridDim.x * blockDim.x) {
+        const bool part = full ? true : presence(g, v) != 0u;
+        flags[v] = part ? (uint8_t)term_init : (uint8_t)0;  // termRound = 1 (program.fs:79)
+    }
+}
+
+// Held + in-flight (s, w) per block (fixed-order partials; the host adds them in order).
+__global__ __launch_bounds__(kBlock) void k_ps_sums(RoundArgs a, uint32_t valid, double2* partials) {
+    __shared__ double2 red[kBlock];
+    double s = 0.0, w = 0.0;
+    for (uint32_t v = blockIdx.x * kBlock + threadIdx.x; v < a.g.actors; v += gridDim.x * kBlock) {
+        uint32_t m;
+        if (!generic_deg(a, v, m)) continue;
+        const uint8_t f = a.flags[v];
+        double2 held = make_double2((double)v, 1.0);
+        if (f & 16u) held = a.frozen[v];
+        else if (valid) held = a.msg_prev[v];
+        s += held.x;
+        w += held.y;
+        if (valid) {
+            const bool sent = a.dir_prev ? a.dir_prev[v] != kDirNone : a.tgt_cur[v] != 0xFFFFFFFFu;
+            if (sent) {
+                const double2 mm = a.msg_prev[v];
+                s += mm.x;
+                w += mm.y;
+            }
+        }
+    }
+    red[threadIdx.x] = make_double2(s, w);
+    __syncthreads();
+    for (int k = kBlock / 2; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) {
+            red[threadIdx.x].x += red[threadIdx.x + k].x;
+            red[threadIdx.x].y += red[threadIdx.x + k].y;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partials[blockIdx.x] = red[0];
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ launchers
+int grid_for(uint32_t n) {
+    uint32_t blocks = (n + kBlock - 1) / kBlock;
+    blocks = (blocks + 7u) & ~7u;  // a multiple of 8: one group per XCD
+    if (blocks < 8) blocks = 8;
+    return (int)(blocks < (uint32_t)kMaxGrid ? blocks : (uint32_t)kMaxGrid);
+}
+
+uint32_t span_for(uint32_t n, int grid) {
+    (void)grid;
+    uint32_t s = (n + 7u) / 8u;
+    return (s + kBlock - 1) / kBlock * kBlock;
+}
+
+void launch_ps_pull(const RoundArgs& a, const Launch& l) {
+    if (a.g.has_link) hipLaunchKernelGGL(k_ps_pull<true>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+    else hipLaunchKernelGGL(k_ps_pull<false>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+}
+
+void launch_gs_pull(const RoundArgs& a, const Launch& l) {
+    if (a.g.has_link) hipLaunchKernelGGL(k_gs_pull<true>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+    else hipLaunchKernelGGL(k_gs_pull<false>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+}
+
+void launch_ps_push_emit(const RoundArgs& a, const Launch& l) {
+    hipLaunchKernelGGL(k_ps_push_emit, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+}
+
+void launch_ps_push_fill(const RoundArgs& a, uint32_t* slot_cur, const uint32_t* boff_cur, const Launch& l) {
+    hipLaunchKernelGGL(k_ps_push_fill, dim3(l.grid), dim3(kBlock), 0, l.stream, a, slot_cur, boff_cur);
+}
+
+void launch_gs_push(const RoundArgs& a, const Launch& l) {
+    hipLaunchKernelGGL(k_gs_push, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+}
+
+void launch_links(uint32_t* link, uint32_t nodes, uint64_t seed, const Launch& l) {
+    hipLaunchKernelGGL(k_links, dim3(l.grid), dim3(kBlock), 0, l.stream, link, nodes, seed);
+}
+
+void launch_count(const uint32_t* idx, uint32_t n, uint32_t* counts, const Launch& l) {
+    hipLaunchKernelGGL(k_count, dim3(l.grid), dim3(kBlock), 0, l.stream, idx, n, counts);
+}
+
+void launch_rev_fill(const uint32_t* link, uint32_t nodes, const uint32_t* rev_off, uint32_t* fillc,
+                     uint32_t* rev_src, const Launch& l) {
+    hipLaunchKernelGGL(k_rev_fill, dim3(l.grid), dim3(kBlock), 0, l.stream, link, nodes, rev_off, fillc, rev_src);
+}
+
+void launch_sort_segments(const uint32_t* off, uint32_t* vals, uint32_t n, const Launch& l) {
+    hipLaunchKernelGGL(k_sort_segments, dim3(l.grid), dim3(kBlock), 0, l.stream, off, vals, n);
+}
+
+size_t scan_scratch_words(uint32_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+
+void launch_exclusive_scan(const uint32_t* in, uint32_t* off, uint32_t n, uint32_t* scratch, hipStream_t s) {
+    const uint32_t nb = (n + kScanTile - 1) / kScanTile;
+    if (nb == 0) return;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kBlock), 0, s, in, n, scratch);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, s, scratch, nb);
+    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kBlock), 0, s, in, off, n, scratch);
+}
+
+void launch_fill_u8(uint8_t* p, uint8_t v, size_t n, hipStream_t s) {
+    size_t blocks = (n + kBlock - 1) / kBlock;
+    if (blocks > (size_t)kMaxGrid) blocks = kMaxGrid;
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(k_fill_u8, dim3((unsigned)blocks), dim3(kBlock), 0, s, p, v, n);
+}
+
+void launch_ps_init(uint8_t* flags, const Geom& g, uint32_t full, uint32_t term_init, const Launch& l) {
+    hipLaunchKernelGGL(k_ps_init, dim3(l.grid), dim3(kBlock), 0, l.stream, flags, g, full, term_init);
+}
+
+void launch_ps_sums(const RoundArgs& a, uint32_t valid, double2* partials, const Launch& l) {
+    hipLaunchKernelGGL(k_ps_sums, dim3(l.grid), dim3(kBlock), 0, l.stream, a, valid, partials);
+}
+
+}  // namespace gp

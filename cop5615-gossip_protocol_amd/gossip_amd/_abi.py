@@ -1,0 +1,91 @@
+"""ctypes binding of libgossip_hip.so (include/gossip_hip.h).
+
+The product path: there is no CPU fallback.  If the HIP library is missing or fails to load,
+import raises — the CPU oracle lives in oracle/ and is test infrastructure only.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libgossip_hip.so")
+HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "gossip_hip.h")
+
+ABI_VERSION = 1
+TOPOLOGIES = {"line": 0, "full": 1, "2D": 2, "Imp3D": 3, "3D": 4}
+ALGOS = {"gossip": 0, "push-sum": 1}
+FLAG_KERNEL_TIMING = 1
+FLAG_GENERIC = 2
+ERRORS = {-1: "GP_EINVAL", -2: "GP_ENOMEM", -3: "GP_EHIP", -4: "GP_ESTATE"}
+
+
+class Config(C.Structure):
+    _fields_ = [("n_arg", C.c_int64), ("topology", C.c_int32), ("algo", C.c_int32),
+                ("seed", C.c_uint64), ("delta", C.c_double), ("gossip_threshold", C.c_int32),
+                ("term_init", C.c_int32), ("term_limit", C.c_int32), ("device", C.c_int32),
+                ("flags", C.c_int32), ("reserved", C.c_int32), ("stream", C.c_void_p)]
+
+
+class Layout(C.Structure):
+    _fields_ = [("nodes", C.c_int64), ("actors", C.c_int64), ("grid", C.c_int64),
+                ("leader", C.c_int64), ("participants", C.c_int64), ("links", C.c_int64),
+                ("device_bytes", C.c_int64)]
+
+
+class Status(C.Structure):
+    _fields_ = [("round", C.c_int64), ("completed", C.c_int64), ("converged", C.c_int32),
+                ("pad", C.c_int32), ("sum_s", C.c_double), ("sum_w", C.c_double),
+                ("device_ms", C.c_double)]
+
+
+class KStats(C.Structure):
+    _fields_ = [("launches", C.c_int64), ("total_ms", C.c_double), ("avg_ms", C.c_double),
+                ("bytes_per_launch", C.c_double), ("kernel", C.c_char * 64)]
+
+
+EXPORTS = ["gp_abi_version", "gp_sizes", "gp_create", "gp_reset", "gp_step", "gp_read_gossip",
+           "gp_read_pushsum", "gp_read_messages", "gp_read_trace", "gp_neighbors",
+           "gp_kernel_stats", "gp_destroy", "gp_last_error"]
+
+
+class GossipError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libgossip_hip.so (raises if absent: build it with `make -C cop5615-gossip_protocol_amd`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GossipError(f"HIP engine not built: {LIB_PATH} missing (run __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    P = C.c_void_p
+    L.gp_abi_version.restype = C.c_int
+    L.gp_sizes.argtypes = [C.c_int64, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.gp_create.argtypes = [C.POINTER(Config), C.POINTER(Layout), C.POINTER(C.c_void_p)]
+    L.gp_reset.argtypes = [P]
+    L.gp_step.argtypes = [P, C.c_int64, C.POINTER(Status)]
+    L.gp_read_gossip.argtypes = [P, C.c_int64, C.c_int64, P, P]
+    L.gp_read_pushsum.argtypes = [P, C.c_int64, C.c_int64, P, P, P]
+    L.gp_read_messages.argtypes = [P, C.c_int64, C.c_int64, P, P, P]
+    L.gp_read_trace.argtypes = [P, C.c_int64, C.c_int64, P]
+    L.gp_neighbors.argtypes = [P, C.c_int64, P, C.c_int32]
+    L.gp_kernel_stats.argtypes = [P, C.POINTER(KStats), C.c_int32]
+    L.gp_destroy.argtypes = [P]
+    L.gp_destroy.restype = None
+    L.gp_last_error.restype = C.c_char_p
+    if L.gp_abi_version() != ABI_VERSION:
+        raise GossipError(f"ABI mismatch: library {L.gp_abi_version()} != {ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = load().gp_last_error().decode(errors="replace")
+        raise GossipError(f"{ERRORS.get(rc, rc)}: {msg}")

@@ -1,0 +1,131 @@
+/*
+ * gossip_hip.h — C ABI of libgossip_hip.so, the MI355X (gfx950) gossip / push-sum engine.
+ *
+ * The reference (/root/reference/program.fs) has no FFI layer: its hot path is fused into the
+ * ChildActor closure (program.fs:74-147), the ParentActor (program.fs:38-67) and the top-level
+ * `match topology` builders (program.fs:150-331).  This ABI is the seam those pieces are cut
+ * at.  Each entry point names the reference code it replaces.
+ *
+ * Conventions
+ *   - plain C, cdecl, blittable POD structs, no C++/torch types;
+ *   - return 0 on success, a negative GP_E* code on failure; gp_last_error() describes it;
+ *   - the library owns every device buffer and its HIP stream (or uses cfg->stream);
+ *     callers own the host buffers passed to gp_read_*;
+ *   - one host thread per handle; a handle is not re-entrant.
+ *
+ * Flag / state encodings shared with the tests and the CPU oracle:
+ *   gossip   flags: bits 0-1 = activation chains (tok, 0..2), bit 2 = done (reported)
+ *   push-sum flags: bits 0-3 = termRound, bit 4 = converged (alreadyConverged)
+ */
+#ifndef GOSSIP_HIP_H
+#define GOSSIP_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GP_ABI_VERSION 1
+
+/* program.fs:151 "line", :191 "full", :227 "2D", :267 "Imp3D"; "3D" is build-defined (Q9) */
+enum gp_topology { GP_LINE = 0, GP_FULL = 1, GP_TWO_D = 2, GP_IMP3D = 3, GP_THREE_D = 4 };
+/* program.fs:177 "gossip", :183 "push-sum" */
+enum gp_algo { GP_GOSSIP = 0, GP_PUSHSUM = 1 };
+
+enum gp_error {
+    GP_OK = 0,
+    GP_EINVAL = -1, /* bad argument / unsupported combination            */
+    GP_ENOMEM = -2, /* device or host allocation failed                  */
+    GP_EHIP = -3,   /* a HIP runtime call failed                         */
+    GP_ESTATE = -4, /* call not valid in the handle's current state      */
+};
+
+enum gp_flags {
+    GP_FLAG_KERNEL_TIMING = 1, /* bracket every round kernel with hipEvents (gp_kernel_stats) */
+    GP_FLAG_GENERIC = 2,       /* force the generic bucketed push path on grid topologies    */
+};
+
+typedef struct gp_config {
+    int64_t n_arg;            /* argv[1] (program.fs:19)                                */
+    int32_t topology;         /* gp_topology, argv[2] (program.fs:20)                   */
+    int32_t algo;             /* gp_algo, argv[3] (program.fs:21)                       */
+    uint64_t seed;            /* Philox4x32-10 key; replaces unseeded Random()          */
+    double delta;             /* push-sum threshold, program.fs:187 (1e-10)             */
+    int32_t gossip_threshold; /* program.fs:102 (10)                                    */
+    int32_t term_init;        /* program.fs:79 (1)                                      */
+    int32_t term_limit;       /* program.fs:135 (3)                                     */
+    int32_t device;           /* HIP device ordinal                                     */
+    int32_t flags;            /* gp_flags                                               */
+    int32_t reserved;
+    void* stream;             /* optional hipStream_t to run on (NULL: library-owned)   */
+} gp_config;
+
+typedef struct gp_layout {
+    int64_t nodes;        /* `nodes` after rounding = completion target (program.fs:27-31,229) */
+    int64_t actors;       /* nodes + 1 actors are spawned (program.fs:152,192,233,269)        */
+    int64_t grid;         /* G (Imp3D/3D, program.fs:268) or g (2D, program.fs:228); else 0   */
+    int64_t leader;       /* program.fs:173/211/250/316                                       */
+    int64_t participants; /* actors with at least one neighbour                              */
+    int64_t links;        /* Imp3D extra links (program.fs:309), 0 otherwise                   */
+    int64_t device_bytes; /* device memory held by the handle                                 */
+} gp_layout;
+
+typedef struct gp_status {
+    int64_t round;     /* synchronous rounds executed                                     */
+    int64_t completed; /* CompletedMessage / PushSumResult count (ParentActor count)       */
+    int32_t converged; /* completed >= nodes (program.fs:49,56)                           */
+    int32_t pad;
+    double sum_s;      /* push-sum: sum of held S plus in-flight s (conservation check)    */
+    double sum_w;      /* push-sum: sum of held W plus in-flight w                         */
+    double device_ms;  /* wall time of the round loop in this gp_step call (hipEvents)     */
+} gp_status;
+
+typedef struct gp_kstats {
+    int64_t launches;   /* round kernels timed since the last reset                         */
+    double total_ms;    /* summed kernel durations                                         */
+    double avg_ms;      /* total_ms / launches                                             */
+    double bytes_per_launch; /* algorithmic HBM bytes of one round kernel    */
+    char kernel[64];    /* name of the dominant round kernel                               */
+} gp_kstats;
+
+int gp_abi_version(void);
+
+/* Node-count rounding of program.fs:26-31 (Imp3D, G from the raw N at :268) and :228-229 (2D). */
+int gp_sizes(int64_t n_arg, int32_t topology, int64_t* nodes, int64_t* actors, int64_t* grid);
+
+/* Replaces the topology builders + actor spawn + InitializeVariables + leader pick
+ * (program.fs:150-175, 191-211, 227-252, 267-317).  Builds the implicit topology and the
+ * Imp3D extra-link CSR on the device and initialises the protocol state. */
+int gp_create(const gp_config* cfg, gp_layout* out, void** handle);
+
+/* Re-initialise protocol state (same topology/links) so a run can be repeated. */
+int gp_reset(void* handle);
+
+/* Replaces the actor message loop (ChildActor, program.fs:82-146) and the ParentActor
+ * termination count (program.fs:44-63): advance at most max_rounds synchronous rounds, or
+ * until completed >= nodes. */
+int gp_step(void* handle, int64_t max_rounds, gp_status* st);
+
+/* State read-back (the caller owns the host buffers; any pointer may be NULL). */
+int gp_read_gossip(void* handle, int64_t first, int64_t count, uint32_t* cnt, uint8_t* flags);
+int gp_read_pushsum(void* handle, int64_t first, int64_t count, double* S, double* W, uint8_t* flags);
+/* Push-sum messages emitted in the last executed round: dst (UINT32_MAX = none), s, w. */
+int gp_read_messages(void* handle, int64_t first, int64_t count, uint32_t* dst, double* s, double* w);
+/* Completion count after each round: completed[i] = count after round first_round + i. */
+int gp_read_trace(void* handle, int64_t first_round, int64_t count, int64_t* completed);
+/* Neighbour list of actor v in the reference's order (program.fs:162-171,201-206,242-248,295-311);
+ * returns the degree (writes at most cap entries) or a negative error. */
+int gp_neighbors(void* handle, int64_t v, uint32_t* out, int32_t cap);
+
+/* Per-kernel timing collected under GP_FLAG_KERNEL_TIMING; reset=1 clears the counters. */
+int gp_kernel_stats(void* handle, gp_kstats* out, int32_t reset);
+
+void gp_destroy(void* handle);
+
+/* Thread-local description of the last failure on this thread. */
+const char* gp_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

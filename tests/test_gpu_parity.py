@@ -1,0 +1,148 @@
+"""GPU parity: the HIP engine (through the C ABI) against the committed golden vectors, the CPU
+oracle on the same seeded inputs, and size-independent properties at BASELINE sizes.
+Bit-exact everywhere: gossip is integer work; push-sum fp64 sums run in the same canonical
+ascending-source order as the oracle (tolerance 0 ulp; north star allows 1e-10 relative)."""
+import numpy as np
+import pytest
+
+import oracle
+from gossip_amd import GossipError, Simulator
+from helpers import bits, check_same, check_state, load_golden, manifest
+
+pytestmark = pytest.mark.gpu
+
+MAN = manifest()
+MID = MAN["mid_rounds"]
+CASES = [c["name"] for c in MAN["cases"]]
+
+
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("generic", [False, True])
+def test_golden(name, generic):
+    g = load_golden(name)
+    topo = [k for k, v in oracle.TOPOLOGIES.items() if v == int(g["topology"])][0]
+    algo = "gossip" if int(g["algo"]) == 0 else "push-sum"
+    sim = Simulator(int(g["n_arg"]), topo, algo, seed=int(g["seed"]), generic=generic)
+    assert (sim.nodes, sim.actors, sim.leader) == (g["nodes"], g["actors"], g["leader"])
+    sim.step(MID)
+    check_state(sim, g, "mid_")
+    st = sim.step(int(g["fin_round"]) - MID)
+    assert st.round == g["fin_round"] and st.converged == g["converged"]
+    np.testing.assert_array_equal(sim.read_trace(), g["trace"])
+    check_state(sim, g, "fin_")
+    sim.close()
+
+
+def _pair(n, topo, algo, seed, **kw):
+    return Simulator(n, topo, algo, seed=seed, **kw), oracle.OracleSim(n, topo, algo, seed=seed)
+
+
+@pytest.mark.parametrize("n,topo,algo,rounds", [
+    (100000, "Imp3D", "push-sum", None),     # to convergence (~540 rounds)
+    (100000, "3D", "push-sum", 400),
+    (100000, "line", "push-sum", 300),
+    (100000, "2D", "push-sum", 200),
+    (20000, "full", "push-sum", None),
+    (100000, "Imp3D", "gossip", None),
+    (100000, "3D", "gossip", None),
+    (3000, "line", "gossip", None),
+    (100000, "full", "gossip", None),
+    (5000, "2D", "gossip", None),
+])
+def test_vs_oracle_100k(n, topo, algo, rounds):
+    gpu, cpu = _pair(n, topo, algo, seed=11)
+    cap = rounds if rounds else 1 << 30
+    # stop at a few intermediate rounds too, so batch boundaries are exercised
+    for chunk in (1, 6, 37):
+        gpu.step(chunk)
+        cpu.step(chunk, threads=8)
+        check_same(gpu, cpu, algo)
+    gs = gpu.step(cap - 44)
+    cs = cpu.step(cap - 44, threads=8)
+    assert (gs.round, gs.completed, gs.converged) == (cs.round, cs.completed, cs.converged)
+    if rounds is None:
+        assert gs.converged
+    check_same(gpu, cpu, algo)
+    if algo == "push-sum":
+        assert gs.sum_s == pytest.approx(cs.sum_s, rel=1e-12)
+        assert gs.sum_w == pytest.approx(cs.sum_w, rel=1e-12)
+
+
+@pytest.mark.parametrize("n,topo", [(1, "line"), (2, "line"), (1, "full"), (2, "full"), (1, "2D"),
+                                    (1, "Imp3D"), (7, "Imp3D"), (8, "Imp3D"), (26, "Imp3D"),
+                                    (8, "3D"), (27, "3D")])
+@pytest.mark.parametrize("algo", ["gossip", "push-sum"])
+def test_edge_sizes(n, topo, algo):
+    gpu, cpu = _pair(n, topo, algo, seed=3)
+    for v in range(gpu.actors):
+        np.testing.assert_array_equal(gpu.neighbors(v), cpu.neighbors(v))
+    gs = gpu.step(3000)
+    cs = cpu.step(3000)
+    assert (gs.round, gs.completed, gs.converged) == (cs.round, cs.completed, cs.converged)
+    check_same(gpu, cpu, algo)
+
+
+def test_3d_single_node_never_converges():
+    """N < 8 in "3D": one node with no neighbours never reports (cap the rounds)."""
+    sim = Simulator(5, "3D", "push-sum")
+    st = sim.step(50)
+    assert st.round == 50 and not st.converged and st.completed == 0
+
+
+def test_neighbors_match_oracle():
+    gpu, cpu = _pair(2000, "Imp3D", "gossip", seed=9)
+    for v in list(range(0, gpu.actors, 37)) + [gpu.actors - 1, gpu.nodes - 1]:
+        np.testing.assert_array_equal(gpu.neighbors(v), cpu.neighbors(v))
+
+
+def test_reset_is_deterministic():
+    sim = Simulator(50000, "Imp3D", "push-sum", seed=2)
+    a = sim.step()
+    S1, W1, f1 = sim.read_pushsum()
+    t1 = sim.read_trace()
+    sim.reset()
+    b = sim.step()
+    S2, W2, f2 = sim.read_pushsum()
+    assert (a.round, a.completed) == (b.round, b.completed)
+    np.testing.assert_array_equal(bits(S1), bits(S2))
+    np.testing.assert_array_equal(f1, f2)
+    np.testing.assert_array_equal(t1, sim.read_trace())
+
+
+def test_imp3d_10m_properties():
+    """BASELINE config 3 at full size: first rounds bit-exact vs the oracle, then
+    size-independent properties to convergence (conservation, monotone trace)."""
+    n = 10_000_000
+    gpu, cpu = _pair(n, "Imp3D", "push-sum", seed=1)
+    assert gpu.nodes == 9_938_375 and gpu.layout.grid == 239
+    gpu.step(12)
+    cpu.step(12, threads=16)
+    check_same(gpu, cpu, "push-sum")
+    cpu.close()
+    want_s = float(gpu.nodes) * (gpu.nodes - 1) / 2.0
+    st = gpu.step()
+    assert st.converged and st.completed >= gpu.nodes
+    assert st.sum_s == pytest.approx(want_s, rel=1e-9)
+    assert st.sum_w == pytest.approx(float(gpu.nodes), rel=1e-9)
+    tr = gpu.read_trace()
+    assert (np.diff(tr) >= 0).all() and tr[-1] >= gpu.nodes and tr[-2] < gpu.nodes
+    S, W, flags = gpu.read_pushsum()
+    assert ((flags[: gpu.nodes] & 16) != 0).all()
+    est = S[: gpu.nodes] / W[: gpu.nodes]
+    assert np.isfinite(est).all()
+    assert abs(np.median(est) - want_s / gpu.nodes) < 0.01 * want_s / gpu.nodes
+
+
+def test_full_gossip_1m_vs_oracle():
+    gpu, cpu = _pair(1_000_000, "full", "gossip", seed=4)
+    gs = gpu.step()
+    cs = cpu.step(threads=16)
+    assert gs.converged and (gs.round, gs.completed) == (cs.round, cs.completed)
+    check_same(gpu, cpu, "gossip")
+
+
+def test_invalid_config_errors():
+    with pytest.raises(GossipError):
+        Simulator(0, "line", "gossip")
+    with pytest.raises(GossipError):
+        Simulator(10, "line", "gossip", term_limit=0)

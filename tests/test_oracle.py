@@ -77,26 +77,7 @@ def test_neighbour_order_line_full_2d():
     assert [list(d.neighbors(v)) for v in range(5)] == [[1], [0, 2], [1, 3], [2, 4], [3]]
 
 
-def _load(name):
-    with np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False) as z:
-        return {k: z[k] for k in z.files}
-
-
-def _check_state(sim, g, prefix):
-    if int(g["algo"]) == 0:
-        cnt, flags = sim.read_gossip()
-        np.testing.assert_array_equal(cnt, g[prefix + "cnt"])
-        np.testing.assert_array_equal(flags, g[prefix + "flags"])
-    else:
-        S, W, flags = sim.read_pushsum()
-        # bit-exact: fp64 in the same canonical order
-        np.testing.assert_array_equal(S.view(np.uint64), g[prefix + "S"].view(np.uint64))
-        np.testing.assert_array_equal(W.view(np.uint64), g[prefix + "W"].view(np.uint64))
-        np.testing.assert_array_equal(flags, g[prefix + "flags"])
-        d, s, w = sim.read_messages()
-        np.testing.assert_array_equal(d, g[prefix + "msg_dst"])
-        np.testing.assert_array_equal(s.view(np.uint64), g[prefix + "msg_s"].view(np.uint64))
-        np.testing.assert_array_equal(w.view(np.uint64), g[prefix + "msg_w"].view(np.uint64))
+from helpers import check_state as _check_state, load_golden as _load  # noqa: E402
 
 
 @pytest.mark.parametrize("name", CASES)
