@@ -83,6 +83,9 @@ struct Handle {
     uint32_t* link = nullptr;
     uint32_t* rev_off = nullptr;
     uint32_t* rev_src = nullptr;
+    uint32_t* lpos = nullptr;
+    uint32_t* ltag[2] = {nullptr, nullptr};
+    double2* lmsg[2] = {nullptr, nullptr};
     // push-sum
     double2* msg[2] = {nullptr, nullptr};
     uint8_t* dir[2] = {nullptr, nullptr};
@@ -156,7 +159,12 @@ struct Handle {
         a.link = link;
         a.rev_off = rev_off;
         a.rev_src = rev_src;
+        a.lpos = lpos;
         const int c = (int)(r & 1u), p = c ^ 1;
+        a.ltag_prev = ltag[p];
+        a.ltag_cur = ltag[c];
+        a.lmsg_prev = lmsg[p];
+        a.lmsg_cur = lmsg[c];
         a.msg_prev = msg[p];
         a.msg_cur = msg[c];
         a.dir_prev = dir[p];
@@ -185,6 +193,12 @@ int build_links(Handle* h) {
     if ((rc = h->alloc(&h->link, nodes))) return rc;
     if ((rc = h->alloc(&h->rev_off, (size_t)A + 1))) return rc;
     if ((rc = h->alloc(&h->rev_src, nodes))) return rc;
+    if (!h->generic) {  // pull kernels: sender-pushed link slots
+        if ((rc = h->alloc(&h->lpos, nodes)) || (rc = h->alloc(&h->ltag[0], nodes)) ||
+            (rc = h->alloc(&h->ltag[1], nodes)))
+            return rc;
+        if (!h->gossip && ((rc = h->alloc(&h->lmsg[0], nodes)) || (rc = h->alloc(&h->lmsg[1], nodes)))) return rc;
+    }
     uint32_t *counts = nullptr, *scratch = nullptr;
     HIP_TRY(hipMalloc(&counts, ((size_t)A + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&scratch, scan_scratch_words(A) * sizeof(uint32_t)));
@@ -200,6 +214,7 @@ int build_links(Handle* h) {
     if (e == hipSuccess) {
         launch_rev_fill(h->link, nodes, h->rev_off, counts, h->rev_src, l);
         launch_sort_segments(h->rev_off, h->rev_src, A, l);  // ascending sources per destination
+        if (h->lpos) launch_lpos(h->rev_src, nodes, h->lpos, l);
         e = hipStreamSynchronize(h->stream);
     }
     if (e == hipSuccess) e = hipGetLastError();
@@ -237,6 +252,8 @@ int reset(Handle* h) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     const size_t A = h->g.actors;
     HIP_TRY(hipMemsetAsync(h->total, 0, (size_t)h->total_cap * sizeof(unsigned long long), h->stream));
+    for (int i = 0; i < 2; ++i)  // no link message in flight (tags never match a round)
+        if (h->ltag[i]) HIP_TRY(hipMemsetAsync(h->ltag[i], 0xFF, (size_t)h->lay.nodes * sizeof(uint32_t), h->stream));
     if (!h->gossip) {
         launch_ps_init(h->flags, h->g, h->full ? 1u : 0u, (uint32_t)h->cfg.term_init, h->L());
         if (h->generic) {
@@ -462,6 +479,8 @@ int gp_create(const gp_config* cfg, gp_layout* out, void** handle) {
         g.wired = (uint32_t)actors;
         g.has_link = 0;
     }
+    g.dx = make_fastdiv(g.gx);
+    g.dy = make_fastdiv(g.gy);
     // leader = Random().Next(0, nodes)  (program.fs:173/211/250/316)
     h->lay.leader = scale_draw(philox(0u, 0u, kStreamLeader, cfg->seed).x, (uint32_t)nodes);
     int64_t part = 0;

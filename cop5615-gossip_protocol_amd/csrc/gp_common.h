@@ -55,12 +55,35 @@ enum Topology { kLine = 0, kFull = 1, kTwoD = 2, kImp3D = 3, kThreeD = 4 };
 // 0:-x 1:+x 2:-y 3:+y 4:-z 5:+z 6:extra link.  7 = no message.
 constexpr uint8_t kDirLink = 6, kDirNone = 7;
 
+// Unsigned 32-bit division by a run-time constant with a precomputed multiplier
+// (Granlund-Montgomery round-up method): q = (t + ((n - t) >> s1)) >> s2, t = mulhi(m, n).
+struct FastDiv {
+    uint32_t d, m, s1, s2;
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+    uint32_t l = 0;
+    while (l < 32 && (1ull << l) < d) ++l;  // l = ceil(log2 d)
+    FastDiv f;
+    f.d = d;
+    f.m = (uint32_t)((((1ull << l) - d) << 32) / d + 1ull);
+    f.s1 = l < 1 ? l : 1u;
+    f.s2 = l > 0 ? l - 1u : 0u;
+    return f;
+}
+
+__host__ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+    const uint32_t t = mulhi32(f.m, n);
+    return (t + ((n - t) >> f.s1)) >> f.s2;
+}
+
 struct Geom {
     uint32_t actors;  // nodes + 1
     uint32_t wired;   // actors with grid neighbours: actors (line/2D) or nodes (Imp3D/3D)
     uint32_t gx, gy, gz;
     uint32_t plane;   // gx * gy
     uint32_t has_link;
+    FastDiv dx, dy;   // division by gx and gy
 };
 
 // Presence mask of v's neighbour list in reference order; bit 6 = extra link.
@@ -68,10 +91,10 @@ struct Geom {
 // z<G-1 && i+G^2<nodes.  line/2D (program.fs:164-169, 244-247) are the gx = actors row.
 __host__ __device__ __forceinline__ uint32_t presence(const Geom& g, uint32_t v) {
     if (v >= g.wired) return 0u;  // the isolated Imp3D actor `nodes` (program.fs:293)
-    const uint32_t x = v % g.gx;
-    const uint32_t yz = v / g.gx;
-    const uint32_t y = yz % g.gy;
-    const uint32_t z = yz / g.gy;
+    const uint32_t yz = fdiv(v, g.dx);
+    const uint32_t x = v - yz * g.gx;
+    const uint32_t z = fdiv(yz, g.dy);
+    const uint32_t y = yz - z * g.gy;
     uint32_t m = 0;
     m |= (x > 0) ? 1u : 0u;
     m |= (x + 1 < g.gx && v + 1 < g.wired) ? 2u : 0u;

@@ -26,6 +26,13 @@ struct RoundArgs {
     const uint32_t* link;     // extra link per wired node (program.fs:309)
     const uint32_t* rev_off;  // CSR of link sources per destination, ascending
     const uint32_t* rev_src;
+    const uint32_t* lpos;     // CSR slot of v's own link edge: rev_src[lpos[v]] == v
+    // extra-link messages are PUSHED by the sender into its CSR slot (ping-pong), tagged with
+    // the round (push-sum) or round*4 + chains (gossip); receivers scan their slots in order.
+    const uint32_t* ltag_prev;
+    uint32_t* ltag_cur;
+    const double2* lmsg_prev;
+    double2* lmsg_cur;
     // push-sum state
     const double2* msg_prev;  // message emitted in round r-1 (= held S,W when not converged)
     double2* msg_cur;
@@ -68,6 +75,7 @@ void launch_count(const uint32_t* idx, uint32_t n, uint32_t* counts, const Launc
 void launch_rev_fill(const uint32_t* link, uint32_t nodes, const uint32_t* rev_off, uint32_t* fillc,
                      uint32_t* rev_src, const Launch& l);
 void launch_sort_segments(const uint32_t* off, uint32_t* vals, uint32_t n, const Launch& l);
+void launch_lpos(const uint32_t* rev_src, uint32_t nlinks, uint32_t* lpos, const Launch& l);
 // exclusive scan of n u32 counts into off[0..n]; scratch >= scan_scratch_words(n) u32
 size_t scan_scratch_words(uint32_t n);
 void launch_exclusive_scan(const uint32_t* in, uint32_t* off, uint32_t n, uint32_t* scratch, hipStream_t s);

@@ -98,6 +98,41 @@ __device__ __forceinline__ PsOut ps_update(uint8_t& f, double2 held, double ss, 
 }
 
 // ------------------------------------------------------------------ push-sum, grid topologies
+// Grid in-neighbour slots in ascending source order: v-P, v-G, v-1, v+1, v+G, v+P (presence
+// bits 4, 2, 0, 1, 3, 5); the sender in slot k targets v iff its direction code is the
+// opposite one (5, 3, 1, 0, 2, 4).
+__device__ __forceinline__ uint32_t slot_src(const Geom& g, uint32_t v, uint32_t k) {
+    switch (k) {
+    case 0: return v - g.plane;
+    case 1: return v - g.gx;
+    case 2: return v - 1u;
+    case 3: return v + 1u;
+    case 4: return v + g.gx;
+    default: return v + g.plane;
+    }
+}
+
+// 6-bit mask of grid in-neighbours whose round r-1 message went to v (slot order).
+template <class Match>
+__device__ __forceinline__ uint32_t grid_hits(const RoundArgs& a, uint32_t v, uint32_t m, Match match) {
+    const Geom& g = a.g;
+    const uint8_t dzm = (m & 16u) ? a.dir_prev[v - g.plane] : (uint8_t)0xFF;
+    const uint8_t dym = (m & 4u) ? a.dir_prev[v - g.gx] : (uint8_t)0xFF;
+    const uint8_t dxm = (m & 1u) ? a.dir_prev[v - 1u] : (uint8_t)0xFF;
+    const uint8_t dxp = (m & 2u) ? a.dir_prev[v + 1u] : (uint8_t)0xFF;
+    const uint8_t dyp = (m & 8u) ? a.dir_prev[v + g.gx] : (uint8_t)0xFF;
+    const uint8_t dzp = (m & 32u) ? a.dir_prev[v + g.plane] : (uint8_t)0xFF;
+    return match(dzm, 5u, 0) | match(dym, 3u, 1) | match(dxm, 1u, 2) | match(dxp, 0u, 3) | match(dyp, 2u, 4) |
+           match(dzp, 4u, 5);
+}
+
+// Link slots scanned with unrolled, predicated loads before the (rare) tail loop.
+constexpr uint32_t kLinkUnroll = 4;
+
+// One actor's round: loads are issued in three dependency levels (own state + neighbour
+// direction bytes + link-slot range -> matched grid messages + link tags/sources -> matched
+// link messages) with no per-lane loops on the common path, so a wave waits ~3 memory
+// latencies per actor instead of one per contribution.
 template <bool LINK>
 __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
     if (ps_gate(a)) return;
@@ -109,59 +144,87 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
     for (; v < end; v += step) {
         const uint32_t m = presence(g, v);
         if (!m) continue;  // non-participant: never sends, never receives
+        // the draw is independent of state: do it first so lpos can be fetched early
+        const uint32_t code = kth_bit(m, scale_draw(philox(v, r, kStreamPush, a.seed).x, popc(m)));
+        // ---- level 1
         uint8_t f = a.flags[v];
+        uint32_t lp = 0;
+        if (LINK && code == kDirLink) lp = a.lpos[v];
+        double2 held = make_double2((double)v, 1.0);  // InitializeVariables (program.fs:107-108)
         double ss = 0.0, ww = 0.0;  // inbox sum from +0.0 in ascending source order
         uint32_t cin = 0;
         if (r) {
-            // directions of the in-neighbours' round r-1 messages (6 independent byte loads)
-            const uint8_t dzm = (m & 16u) ? a.dir_prev[v - g.plane] : kDirNone;
-            const uint8_t dym = (m & 4u) ? a.dir_prev[v - g.gx] : kDirNone;
-            const uint8_t dxm = (m & 1u) ? a.dir_prev[v - 1u] : kDirNone;
-            const uint8_t dxp = (m & 2u) ? a.dir_prev[v + 1u] : kDirNone;
-            const uint8_t dyp = (m & 8u) ? a.dir_prev[v + g.gx] : kDirNone;
-            const uint8_t dzp = (m & 32u) ? a.dir_prev[v + g.plane] : kDirNone;
-            uint32_t li = 0, le = 0;
+            if (!(f & 16u)) held = a.msg_prev[v];
+            uint32_t hits = grid_hits(a, v, m, [](uint8_t d, uint32_t c, int k) { return d == c ? 1u << k : 0u; });
+            uint32_t li = 0, nl = 0;
             if (LINK) {
                 li = a.rev_off[v];
-                le = a.rev_off[v + 1];
+                nl = a.rev_off[v + 1] - li;
             }
-            auto take = [&](uint32_t u) {
-                const double2 mm = a.msg_prev[u];
+            // ---- level 2: grid messages that hit v, link tags + sources
+            double2 gm[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                gm[k] = make_double2(0.0, 0.0);
+                if (hits & (1u << k)) gm[k] = a.msg_prev[slot_src(g, v, (uint32_t)k)];
+            }
+            auto add = [&](double2 mm) {
                 ss += mm.x;
                 ww += mm.y;
                 ++cin;
             };
-            // link sources below `bound`, in ascending order (duplicates of a grid neighbour
-            // are harmless: a sender's single code matches at most one of the two entries)
+            // add pending grid messages from sources below `bound` (slots are ascending)
             auto flush = [&](uint32_t bound) {
-                if (LINK) {
-                    while (li < le) {
-                        const uint32_t s = a.rev_src[li];
-                        if (s >= bound) break;
-                        if (a.dir_prev[s] == kDirLink) take(s);
-                        ++li;
+#pragma unroll
+                for (int k = 0; k < 6; ++k)
+                    if ((hits & (1u << k)) && slot_src(g, v, (uint32_t)k) < bound) {
+                        add(gm[k]);
+                        hits &= ~(1u << k);
+                    }
+            };
+            if (LINK) {
+                uint32_t lt[kLinkUnroll], ls[kLinkUnroll];
+#pragma unroll
+                for (uint32_t k = 0; k < kLinkUnroll; ++k) {
+                    lt[k] = 0xFFFFFFFFu;
+                    ls[k] = 0;
+                    if (k < nl) {
+                        lt[k] = a.ltag_prev[li + k];
+                        ls[k] = a.rev_src[li + k];
                     }
                 }
-            };
-            if (m & 16u) { flush(v - g.plane); if (dzm == 5) take(v - g.plane); }
-            if (m & 4u) { flush(v - g.gx); if (dym == 3) take(v - g.gx); }
-            if (m & 1u) { flush(v - 1u); if (dxm == 1) take(v - 1u); }
-            if (m & 2u) { flush(v + 1u); if (dxp == 0) take(v + 1u); }
-            if (m & 8u) { flush(v + g.gx); if (dyp == 2) take(v + g.gx); }
-            if (m & 32u) { flush(v + g.plane); if (dzp == 4) take(v + g.plane); }
+                // ---- level 3: matched link messages
+                double2 lm[kLinkUnroll];
+#pragma unroll
+                for (uint32_t k = 0; k < kLinkUnroll; ++k) {
+                    lm[k] = make_double2(0.0, 0.0);
+                    if (lt[k] == r - 1u) lm[k] = a.lmsg_prev[li + k];
+                }
+                // merge: link slots are sorted by source; a sender matches grid OR link, never both
+#pragma unroll
+                for (uint32_t k = 0; k < kLinkUnroll; ++k)
+                    if (lt[k] == r - 1u) {
+                        flush(ls[k]);
+                        add(lm[k]);
+                    }
+                for (uint32_t k = kLinkUnroll; k < nl; ++k)  // rare: more than kLinkUnroll sources
+                    if (a.ltag_prev[li + k] == r - 1u) {
+                        flush(a.rev_src[li + k]);
+                        add(a.lmsg_prev[li + k]);
+                    }
+            }
             flush(0xFFFFFFFFu);
         }
-        double2 held;
-        if (!(f & 16u)) held = r ? a.msg_prev[v] : make_double2((double)v, 1.0);  // InitializeVariables
         const uint8_t f0 = f;
         const PsOut o = ps_update(f, held, ss, ww, cin, a.delta, a.term_limit);
-        uint8_t code = kDirNone;
         if (o.send) {
-            const uint4 x = philox(v, r, kStreamPush, a.seed);
-            code = (uint8_t)kth_bit(m, scale_draw(x.x, popc(m)));
             a.msg_cur[v] = o.msg;
+            if (LINK && code == kDirLink) {
+                a.lmsg_cur[lp] = o.msg;
+                a.ltag_cur[lp] = r;
+            }
         }
-        a.dir_cur[v] = code;
+        a.dir_cur[v] = o.send ? (uint8_t)code : kDirNone;
         if (f != f0) a.flags[v] = f;
         if (o.conv_now) {
             a.frozen[v] = o.msg;
@@ -172,6 +235,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
 }
 
 // ------------------------------------------------------------------ gossip, grid topologies
+// dir byte = chain-0 code | chain-1 code << 4 (15 = no chain)
 __device__ __forceinline__ uint32_t nib_match(uint8_t b, uint32_t code) {
     return (uint32_t)((b & 15u) == code) + (uint32_t)((b >> 4) == code);
 }
@@ -199,8 +263,16 @@ __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
             if (m & 8u) inc += nib_match(a.dir_prev[v + g.gx], 2);
             if (m & 32u) inc += nib_match(a.dir_prev[v + g.plane], 4);
             if (LINK) {
-                const uint32_t le = a.rev_off[v + 1];
-                for (uint32_t li = a.rev_off[v]; li < le; ++li) inc += nib_match(a.dir_prev[a.rev_src[li]], kDirLink);
+                const uint32_t li = a.rev_off[v], nl = a.rev_off[v + 1] - li;
+#pragma unroll
+                for (uint32_t k = 0; k < kLinkUnroll; ++k) {
+                    const uint32_t t = k < nl ? a.ltag_prev[li + k] : 0xFFFFFFFFu;
+                    if ((t >> 2) == r - 1u) inc += t & 3u;
+                }
+                for (uint32_t k = kLinkUnroll; k < nl; ++k) {
+                    const uint32_t t = a.ltag_prev[li + k];
+                    if ((t >> 2) == r - 1u) inc += t & 3u;
+                }
             }
             if (inc) {
                 const uint32_t c0 = a.cnt[v], c1 = c0 + inc;
@@ -219,6 +291,10 @@ __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
             const uint32_t c0 = kth_bit(m, scale_draw(x.x, d));
             const uint32_t c1 = tok > 1 ? kth_bit(m, scale_draw(x.y, d)) : 15u;
             a.dir_cur[v] = (uint8_t)(c0 | (c1 << 4));
+            if (LINK) {
+                const uint32_t nl = (uint32_t)(c0 == kDirLink) + (uint32_t)(c1 == kDirLink);
+                if (nl) a.ltag_cur[a.lpos[v]] = r * 4u + nl;
+            }
         }
     }
     if (r) block_add(newly, &a.total[r - 1]);
@@ -382,6 +458,11 @@ __global__ void k_sort_segments(const uint32_t* off, uint32_t* vals, uint32_t n)
             vals[j] = x;
         }
     }
+}
+
+__global__ void k_lpos(const uint32_t* rev_src, uint32_t nlinks, uint32_t* lpos) {
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < nlinks; p += gridDim.x * blockDim.x)
+        lpos[rev_src[p]] = p;
 }
 
 constexpr uint32_t kScanPer = 8;
@@ -554,6 +635,10 @@ void launch_rev_fill(const uint32_t* link, uint32_t nodes, const uint32_t* rev_o
 
 void launch_sort_segments(const uint32_t* off, uint32_t* vals, uint32_t n, const Launch& l) {
     hipLaunchKernelGGL(k_sort_segments, dim3(l.grid), dim3(kBlock), 0, l.stream, off, vals, n);
+}
+
+void launch_lpos(const uint32_t* rev_src, uint32_t nlinks, uint32_t* lpos, const Launch& l) {
+    hipLaunchKernelGGL(k_lpos, dim3(l.grid), dim3(kBlock), 0, l.stream, rev_src, nlinks, lpos);
 }
 
 size_t scan_scratch_words(uint32_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
