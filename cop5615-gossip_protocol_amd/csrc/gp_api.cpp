@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -84,8 +85,8 @@ struct Handle {
     uint32_t* rev_off = nullptr;
     uint32_t* rev_src = nullptr;
     uint32_t* lpos = nullptr;
-    uint32_t* ltag[2] = {nullptr, nullptr};
-    double2* lmsg[2] = {nullptr, nullptr};
+    uint8_t* lcnt[2] = {nullptr, nullptr};   // gossip link slots
+    double2* lmsg[2] = {nullptr, nullptr};   // push-sum link slots
     // push-sum
     double2* msg[2] = {nullptr, nullptr};
     uint8_t* dir[2] = {nullptr, nullptr};
@@ -105,6 +106,7 @@ struct Handle {
     // control
     unsigned long long* total = nullptr;
     int64_t total_cap = 0;
+    uint32_t* parts = nullptr;
     double2* partials = nullptr;
     unsigned long long* h_trace = nullptr;  // pinned
     int64_t h_trace_cap = 0;
@@ -113,6 +115,7 @@ struct Handle {
     int64_t completed = 0;
     bool converged = false;
     int64_t batch = 8;
+    uint32_t ablate = 0;  // DEBUG: GP_ABLATE env var (cost attribution only; breaks results)
     // timing
     std::vector<hipEvent_t> kev;
     hipEvent_t ev_a = nullptr, ev_b = nullptr;
@@ -155,14 +158,16 @@ struct Handle {
         a.threshold = (uint32_t)cfg.gossip_threshold;
         a.delta = cfg.delta;
         a.term_limit = (uint32_t)cfg.term_limit;
+        a.ablate = ablate;
         a.total = total;
+        a.parts = parts;
         a.link = link;
         a.rev_off = rev_off;
         a.rev_src = rev_src;
         a.lpos = lpos;
         const int c = (int)(r & 1u), p = c ^ 1;
-        a.ltag_prev = ltag[p];
-        a.ltag_cur = ltag[c];
+        a.lcnt_prev = lcnt[p];
+        a.lcnt_cur = lcnt[c];
         a.lmsg_prev = lmsg[p];
         a.lmsg_cur = lmsg[c];
         a.msg_prev = msg[p];
@@ -194,10 +199,12 @@ int build_links(Handle* h) {
     if ((rc = h->alloc(&h->rev_off, (size_t)A + 1))) return rc;
     if ((rc = h->alloc(&h->rev_src, nodes))) return rc;
     if (!h->generic) {  // pull kernels: sender-pushed link slots
-        if ((rc = h->alloc(&h->lpos, nodes)) || (rc = h->alloc(&h->ltag[0], nodes)) ||
-            (rc = h->alloc(&h->ltag[1], nodes)))
+        if ((rc = h->alloc(&h->lpos, nodes))) return rc;
+        if (h->gossip) {
+            if ((rc = h->alloc(&h->lcnt[0], nodes)) || (rc = h->alloc(&h->lcnt[1], nodes))) return rc;
+        } else if ((rc = h->alloc(&h->lmsg[0], nodes)) || (rc = h->alloc(&h->lmsg[1], nodes))) {
             return rc;
-        if (!h->gossip && ((rc = h->alloc(&h->lmsg[0], nodes)) || (rc = h->alloc(&h->lmsg[1], nodes)))) return rc;
+        }
     }
     uint32_t *counts = nullptr, *scratch = nullptr;
     HIP_TRY(hipMalloc(&counts, ((size_t)A + 1) * sizeof(uint32_t)));
@@ -252,8 +259,11 @@ int reset(Handle* h) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     const size_t A = h->g.actors;
     HIP_TRY(hipMemsetAsync(h->total, 0, (size_t)h->total_cap * sizeof(unsigned long long), h->stream));
-    for (int i = 0; i < 2; ++i)  // no link message in flight (tags never match a round)
-        if (h->ltag[i]) HIP_TRY(hipMemsetAsync(h->ltag[i], 0xFF, (size_t)h->lay.nodes * sizeof(uint32_t), h->stream));
+    HIP_TRY(hipMemsetAsync(h->parts, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t), h->stream));
+    for (int i = 0; i < 2; ++i) {  // no link message in flight
+        if (h->lcnt[i]) HIP_TRY(hipMemsetAsync(h->lcnt[i], 0, (size_t)h->lay.nodes, h->stream));
+        if (h->lmsg[i]) launch_fill_empty_slots(h->lmsg[i], (size_t)h->lay.nodes, h->stream);
+    }
     if (!h->gossip) {
         launch_ps_init(h->flags, h->g, h->full ? 1u : 0u, (uint32_t)h->cfg.term_init, h->L());
         if (h->generic) {
@@ -300,15 +310,19 @@ const char* round_kernel_name(const Handle* h) {
 }
 
 // Algorithmic (compulsory) HBM bytes of one round kernel; DESIGN.md §5.
+//   push-sum pull: held (S,W) read 16 + message write 16 + direction byte write 1 + own
+//   direction/flag bytes read 2 per participant; Imp3D adds the link CSR (rev_off 4 per actor,
+//   source id 4 + slot 16 per link) and the pushed link message (16 per sender choosing it).
 double bytes_per_round(const Handle* h) {
     const double P = (double)h->lay.participants, A = (double)h->lay.actors, links = (double)h->lay.links;
     if (h->gossip) {
         if (h->generic) return P * (4 + 4 + 1 + 1) + P * 2 * 4;  // cnt r/w, inc r, state r/w, 2 atomics
-        return P * (1 + 1 + 1) + (h->g.has_link ? 4 * A + 4 * links : 0);  // state r, dir r, dir w
+        return P * (1 + 1 + 1) + (h->g.has_link ? 4 * A + 1 * links : 0);  // state r, dir r, dir w
     }
     if (h->generic) return P * (16 + 16 + 16 + 1 + 4 + 4 + 4 + 4 + 4);
-    // msg_prev read once (16), msg_cur write (16), dir r/w (2), flags r (1)
-    return P * (16 + 16 + 2 + 1) + (h->g.has_link ? 4 * A + 4 * links : 0);
+    double b = P * (16 + 16 + 1 + 2);
+    if (h->g.has_link) b += 4 * A + links * (4 + 16) + 16.0 * links / 7.0;
+    return b;
 }
 
 int launch_round(Handle* h, int64_t k) {
@@ -356,8 +370,10 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
             if ((rc = launch_round(h, h->next_kernel + i))) return rc;
             if (timing) HIP_TRY(hipEventRecord(h->kev[2 * i + 1], h->stream));
         }
-        HIP_TRY(hipGetLastError());
         h->next_kernel += B;
+        // total[] of the last round this batch applied (F(k) applies round k, or k-1 for gossip)
+        launch_finalize(h->total, h->parts, h->next_kernel - (h->gossip ? 2 : 1), h->stream);
+        HIP_TRY(hipGetLastError());
         // total[] entries of the rounds completed by this batch
         if (B > h->h_trace_cap) {
             if (h->h_trace) (void)hipHostFree(h->h_trace);
@@ -488,7 +504,12 @@ int gp_create(const gp_config* cfg, gp_layout* out, void** handle) {
     else
         for (int64_t v = 0; v < actors; ++v) part += presence(g, (uint32_t)v) != 0u;
     h->lay.participants = part;
+    if (const char* ab = std::getenv("GP_ABLATE")) h->ablate = (uint32_t)std::strtoul(ab, nullptr, 0);
     h->grid = grid_for(g.actors);
+    if (const char* gg = std::getenv("GP_GRID")) {  // tuning override (rounded to a multiple of 8)
+        const long v = std::strtol(gg, nullptr, 0);
+        if (v >= 8) h->grid = (int)((v + 7) / 8 * 8);
+    }
     h->span = span_for(g.actors, h->grid);
 
     auto bail = [&](int code) {
@@ -530,6 +551,7 @@ int gp_create(const gp_config* cfg, gp_layout* out, void** handle) {
         }
     }
     if (g.has_link && (rc = build_links(h))) return bail(rc);
+    if ((rc = h->alloc(&h->parts, (size_t)kPartRing * kParts * kPartStride))) return bail(rc);
     if ((rc = ensure_trace(h, 4096))) return bail(rc);
     if ((rc = reset(h))) return bail(rc);
     h->lay.device_bytes = (int64_t)h->dev_bytes;

@@ -5,7 +5,12 @@
 namespace gp {
 
 constexpr int kBlock = 256;       // 4 waves of 64
-constexpr int kMaxGrid = 256 * 8; // 256 CUs x 8 workgroups: grid-stride beyond that
+constexpr int kMaxGrid = 256 * 16; // 256 CUs x 16 workgroups: grid-stride beyond that
+constexpr int kParts = 64;          // completion sub-counters per round (one 64 B line each)
+constexpr int kPartStride = 16;     // u32 words between sub-counters
+constexpr int kPartRing = 4;        // rounds kept in the sub-counter ring
+// empty link slot: w holds this quiet-NaN bit pattern (a real weight is finite and >= 0)
+constexpr unsigned long long kEmptySlot = 0x7FF800000000DEADull;
 
 // One synchronous round kernel F(r) fuses phase 2 of round r-1 (collect the messages sent to
 // this actor, read from the round r-1 buffers) with phase 1 of round r (update, convergence
@@ -21,17 +26,20 @@ struct RoundArgs {
     uint32_t threshold;    // gossip report threshold (program.fs:102)
     double delta;          // push-sum delta (program.fs:187)
     uint32_t term_limit;   // program.fs:135
-    unsigned long long* total;  // total[r] = completion count after round r (trace)
+    uint32_t ablate;       // DEBUG ONLY (env GP_ABLATE): bits skip work for cost attribution; results invalid
+    unsigned long long* total;  // total[a] = completion count after round a (trace)
+    uint32_t* parts;            // kPartRing x kParts padded sub-counters of newly reported actors
     // topology side data (Imp3D)
     const uint32_t* link;     // extra link per wired node (program.fs:309)
     const uint32_t* rev_off;  // CSR of link sources per destination, ascending
     const uint32_t* rev_src;
     const uint32_t* lpos;     // CSR slot of v's own link edge: rev_src[lpos[v]] == v
-    // extra-link messages are PUSHED by the sender into its CSR slot (ping-pong), tagged with
-    // the round (push-sum) or round*4 + chains (gossip); receivers scan their slots in order.
-    const uint32_t* ltag_prev;
-    uint32_t* ltag_cur;
-    const double2* lmsg_prev;
+    // extra-link messages are PUSHED by the sender into its CSR slot (ping-pong); the receiver
+    // scans its slots in order and empties what it consumed (push-sum: w = kEmptySlot NaN;
+    // gossip: a u8 chain count set back to 0).
+    uint8_t* lcnt_prev;
+    uint8_t* lcnt_cur;
+    double2* lmsg_prev;
     double2* lmsg_cur;
     // push-sum state
     const double2* msg_prev;  // message emitted in round r-1 (= held S,W when not converged)
@@ -80,6 +88,9 @@ void launch_lpos(const uint32_t* rev_src, uint32_t nlinks, uint32_t* lpos, const
 size_t scan_scratch_words(uint32_t n);
 void launch_exclusive_scan(const uint32_t* in, uint32_t* off, uint32_t n, uint32_t* scratch, hipStream_t s);
 void launch_fill_u8(uint8_t* p, uint8_t v, size_t n, hipStream_t s);
+void launch_fill_empty_slots(double2* p, size_t n, hipStream_t s);
+// total[a] = total[a-1] + sum of the round-a sub-counters (after the last kernel of a batch)
+void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hipStream_t s);
 void launch_ps_init(uint8_t* flags, const Geom& g, uint32_t full, uint32_t term_init, const Launch& l);
 // push-sum sums for gp_status: per-block partials of held + in-flight (s, w)
 void launch_ps_sums(const RoundArgs& a, uint32_t last_round_valid, double2* partials, const Launch& l);

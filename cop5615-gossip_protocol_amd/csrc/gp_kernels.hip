@@ -32,8 +32,13 @@ __device__ __forceinline__ void node_range(uint32_t n, uint32_t span, uint32_t& 
     step = per * kBlock;
 }
 
-// Block-wide sum of one u32 per thread; thread 0 adds it to *dst when nonzero.
-__device__ __forceinline__ void block_add(uint32_t c, unsigned long long* dst) {
+__device__ __forceinline__ uint32_t* part_slot(uint32_t* parts, long long a, uint32_t j) {
+    return parts + ((uint32_t)(a & (kPartRing - 1)) * kParts + j) * kPartStride;
+}
+
+// Block-wide sum of one u32 per thread; thread 0 adds it to this block's sub-counter of
+// round `a` (64 sub-counters on separate lines: no single-address atomic contention).
+__device__ __forceinline__ void block_add(uint32_t c, uint32_t* parts, long long a) {
     __shared__ uint32_t red[kBlock / 64];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
@@ -43,24 +48,30 @@ __device__ __forceinline__ void block_add(uint32_t c, unsigned long long* dst) {
         uint32_t t = 0;
 #pragma unroll
         for (int i = 0; i < kBlock / 64; ++i) t += red[i];
-        if (t) atomicAdd(dst, (unsigned long long)t);
+        if (t) atomicAdd(part_slot(parts, a, blockIdx.x & (kParts - 1)), t);
     }
 }
 
-// Push-sum skip gate.  total[r-1] is final (written by earlier launches), so every block takes
-// the same branch; block 0 seeds total[r] with it so the count stays cumulative even when the
-// round is skipped after convergence.
-__device__ __forceinline__ bool ps_gate(const RoundArgs& a) {
-    const unsigned long long prev = a.r ? a.total[a.r - 1] : 0ull;
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&a.total[a.r], prev);
-    return prev >= a.target;
-}
-
-// Gossip skip gate: F(r) applies round r-1, so it seeds total[r-1] with total[r-2].
-__device__ __forceinline__ bool gs_gate(const RoundArgs& a) {
-    const unsigned long long prev = a.r >= 2 ? a.total[a.r - 2] : 0ull;
-    if (a.r >= 1 && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&a.total[a.r - 1], prev);
-    return prev >= a.target;
+// Skip gate of a kernel that applies round `a`: the completion count after round a-1 is
+// total[a-2] + the round a-1 sub-counters, all final (earlier launches).  Every block computes
+// it (one wave, 64 loads), so every block takes the same branch; block 0 publishes total[a-1]
+// and empties the ring slot that round a+2 will use.
+__device__ __forceinline__ bool gate(const RoundArgs& A, long long a) {
+    __shared__ unsigned long long prev_s;
+    if (threadIdx.x < 64) {
+        unsigned long long x = 0;
+        if (a >= 1) x = *part_slot(A.parts, a - 1, threadIdx.x);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        if (threadIdx.x == 0) {
+            if (a >= 2) x += A.total[a - 2];
+            prev_s = x;
+            if (blockIdx.x == 0 && a >= 1) A.total[a - 1] = x;
+        }
+        if (blockIdx.x == 0) *part_slot(A.parts, a + 2, threadIdx.x) = 0u;
+    }
+    __syncthreads();
+    return prev_s >= A.target;
 }
 
 // program.fs:119-143 for one actor (round 0 = :110-116): absorb, test, halve, emit.
@@ -112,30 +123,33 @@ __device__ __forceinline__ uint32_t slot_src(const Geom& g, uint32_t v, uint32_t
     }
 }
 
-// 6-bit mask of grid in-neighbours whose round r-1 message went to v (slot order).
-template <class Match>
-__device__ __forceinline__ uint32_t grid_hits(const RoundArgs& a, uint32_t v, uint32_t m, Match match) {
-    const Geom& g = a.g;
-    const uint8_t dzm = (m & 16u) ? a.dir_prev[v - g.plane] : (uint8_t)0xFF;
-    const uint8_t dym = (m & 4u) ? a.dir_prev[v - g.gx] : (uint8_t)0xFF;
-    const uint8_t dxm = (m & 1u) ? a.dir_prev[v - 1u] : (uint8_t)0xFF;
-    const uint8_t dxp = (m & 2u) ? a.dir_prev[v + 1u] : (uint8_t)0xFF;
-    const uint8_t dyp = (m & 8u) ? a.dir_prev[v + g.gx] : (uint8_t)0xFF;
-    const uint8_t dzp = (m & 32u) ? a.dir_prev[v + g.plane] : (uint8_t)0xFF;
-    return match(dzm, 5u, 0) | match(dym, 3u, 1) | match(dxm, 1u, 2) | match(dxp, 0u, 3) | match(dyp, 2u, 4) |
-           match(dzp, 4u, 5);
+// Slot k of v exists iff presence bit kSlotBit(k) is set; its sender targets v iff its
+// direction code is kSlotCode(k).
+__device__ __forceinline__ uint32_t slot_bit(uint32_t k) { return k == 0 ? 16u : k == 1 ? 4u : k == 2 ? 1u : k == 3 ? 2u : k == 4 ? 8u : 32u; }
+__device__ __forceinline__ uint32_t slot_code(uint32_t k) { return k == 0 ? 5u : k == 1 ? 3u : k == 2 ? 1u : k == 3 ? 0u : k == 4 ? 2u : 4u; }
+
+// Branch-free load: a predicated-off lane reads `fallback` (an element it already touches),
+// so hipcc emits straight-line loads instead of one basic block + vmcnt(0) per condition.
+template <class T>
+__device__ __forceinline__ T load_sel(const T* base, bool pred, uint32_t idx, uint32_t fallback) {
+    return base[pred ? idx : fallback];
 }
 
-// Link slots scanned with unrolled, predicated loads before the (rare) tail loop.
+// Link slots scanned with unrolled loads before the (rare) tail loop.
 constexpr uint32_t kLinkUnroll = 4;
 
-// One actor's round: loads are issued in three dependency levels (own state + neighbour
-// direction bytes + link-slot range -> matched grid messages + link tags/sources -> matched
-// link messages) with no per-lane loops on the common path, so a wave waits ~3 memory
-// latencies per actor instead of one per contribution.
+__device__ __forceinline__ bool slot_full(double2 m) {
+    return (unsigned long long)__double_as_longlong(m.y) != kEmptySlot;
+}
+
+// One actor's round.  All loads are unconditional (clamped addresses) and issued in two
+// dependency levels: (1) own flags + held (S,W), the six neighbours' direction bytes, the
+// link-slot range; (2) the grid messages that hit v and the first kLinkUnroll link slots
+// (each a 16-byte message written by its sender, or the empty marker) with their source
+// ids.  Consumed link slots are emptied for reuse two rounds later.
 template <bool LINK>
 __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
-    if (ps_gate(a)) return;
+    if (gate(a, a.r)) return;
     const Geom g = a.g;
     const uint32_t r = a.r;
     uint32_t v, end, step;
@@ -145,29 +159,33 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
         const uint32_t m = presence(g, v);
         if (!m) continue;  // non-participant: never sends, never receives
         // the draw is independent of state: do it first so lpos can be fetched early
-        const uint32_t code = kth_bit(m, scale_draw(philox(v, r, kStreamPush, a.seed).x, popc(m)));
+        const uint32_t code = (a.ablate & 8u) ? kth_bit(m, v % popc(m))
+                                              : kth_bit(m, scale_draw(philox(v, r, kStreamPush, a.seed).x, popc(m)));
         // ---- level 1
         uint8_t f = a.flags[v];
         uint32_t lp = 0;
-        if (LINK && code == kDirLink) lp = a.lpos[v];
+        if (LINK) lp = load_sel(a.lpos, code == kDirLink, v, 0u);
         double2 held = make_double2((double)v, 1.0);  // InitializeVariables (program.fs:107-108)
         double ss = 0.0, ww = 0.0;  // inbox sum from +0.0 in ascending source order
         uint32_t cin = 0;
         if (r) {
-            if (!(f & 16u)) held = a.msg_prev[v];
-            uint32_t hits = grid_hits(a, v, m, [](uint8_t d, uint32_t c, int k) { return d == c ? 1u << k : 0u; });
+            held = a.msg_prev[v];
+            uint8_t d[6];
+#pragma unroll
+            for (uint32_t k = 0; k < 6; ++k) d[k] = load_sel(a.dir_prev, (m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
             uint32_t li = 0, nl = 0;
             if (LINK) {
                 li = a.rev_off[v];
-                nl = a.rev_off[v + 1] - li;
+                nl = (a.ablate & 1u) ? 0u : a.rev_off[v + 1] - li;
             }
-            // ---- level 2: grid messages that hit v, link tags + sources
+            uint32_t hits = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 6; ++k) hits |= ((m & slot_bit(k)) && d[k] == slot_code(k)) ? 1u << k : 0u;
+            if (a.ablate & 16u) hits = 0;
+            // ---- level 2
             double2 gm[6];
 #pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                gm[k] = make_double2(0.0, 0.0);
-                if (hits & (1u << k)) gm[k] = a.msg_prev[slot_src(g, v, (uint32_t)k)];
-            }
+            for (uint32_t k = 0; k < 6; ++k) gm[k] = load_sel(a.msg_prev, (hits >> k) & 1u, slot_src(g, v, k), v);
             auto add = [&](double2 mm) {
                 ss += mm.x;
                 ww += mm.y;
@@ -176,42 +194,36 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
             // add pending grid messages from sources below `bound` (slots are ascending)
             auto flush = [&](uint32_t bound) {
 #pragma unroll
-                for (int k = 0; k < 6; ++k)
-                    if ((hits & (1u << k)) && slot_src(g, v, (uint32_t)k) < bound) {
+                for (uint32_t k = 0; k < 6; ++k)
+                    if ((hits & (1u << k)) && slot_src(g, v, k) < bound) {
                         add(gm[k]);
                         hits &= ~(1u << k);
                     }
             };
             if (LINK) {
-                uint32_t lt[kLinkUnroll], ls[kLinkUnroll];
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k) {
-                    lt[k] = 0xFFFFFFFFu;
-                    ls[k] = 0;
-                    if (k < nl) {
-                        lt[k] = a.ltag_prev[li + k];
-                        ls[k] = a.rev_src[li + k];
-                    }
-                }
-                // ---- level 3: matched link messages
                 double2 lm[kLinkUnroll];
+                uint32_t ls[kLinkUnroll];
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) {
-                    lm[k] = make_double2(0.0, 0.0);
-                    if (lt[k] == r - 1u) lm[k] = a.lmsg_prev[li + k];
+                    lm[k] = load_sel(a.lmsg_prev, k < nl, li + k, 0u);
+                    ls[k] = load_sel(a.rev_src, k < nl, li + k, 0u);
                 }
                 // merge: link slots are sorted by source; a sender matches grid OR link, never both
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k)
-                    if (lt[k] == r - 1u) {
+                    if (k < nl && slot_full(lm[k])) {
                         flush(ls[k]);
                         add(lm[k]);
+                        a.lmsg_prev[li + k].y = __longlong_as_double((long long)kEmptySlot);
                     }
-                for (uint32_t k = kLinkUnroll; k < nl; ++k)  // rare: more than kLinkUnroll sources
-                    if (a.ltag_prev[li + k] == r - 1u) {
+                for (uint32_t k = kLinkUnroll; k < nl; ++k) {  // rare: more than kLinkUnroll sources
+                    const double2 mm = a.lmsg_prev[li + k];
+                    if (slot_full(mm)) {
                         flush(a.rev_src[li + k]);
-                        add(a.lmsg_prev[li + k]);
+                        add(mm);
+                        a.lmsg_prev[li + k].y = __longlong_as_double((long long)kEmptySlot);
                     }
+                }
             }
             flush(0xFFFFFFFFu);
         }
@@ -219,10 +231,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
         const PsOut o = ps_update(f, held, ss, ww, cin, a.delta, a.term_limit);
         if (o.send) {
             a.msg_cur[v] = o.msg;
-            if (LINK && code == kDirLink) {
-                a.lmsg_cur[lp] = o.msg;
-                a.ltag_cur[lp] = r;
-            }
+            if (LINK && code == kDirLink && !(a.ablate & 4u)) a.lmsg_cur[lp] = o.msg;
         }
         a.dir_cur[v] = o.send ? (uint8_t)code : kDirNone;
         if (f != f0) a.flags[v] = f;
@@ -231,7 +240,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
             ++newly;
         }
     }
-    block_add(newly, &a.total[r]);
+    block_add(newly, a.parts, r);
 }
 
 // ------------------------------------------------------------------ gossip, grid topologies
@@ -242,7 +251,7 @@ __device__ __forceinline__ uint32_t nib_match(uint8_t b, uint32_t code) {
 
 template <bool LINK>
 __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
-    if (gs_gate(a)) return;
+    if (a.r && gate(a, (long long)a.r - 1)) return;
     const Geom g = a.g;
     const uint32_t r = a.r;
     uint32_t v, end, step;
@@ -255,23 +264,29 @@ __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
         uint32_t tok = st & 3u;
         uint32_t done = (st >> 2) & 1u;
         if (r && !done) {  // apply round r-1: receipts while not done at round start (program.fs:92)
+            uint8_t d[6];
+#pragma unroll
+            for (uint32_t k = 0; k < 6; ++k) d[k] = load_sel(a.dir_prev, (m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
             uint32_t inc = 0;
-            if (m & 16u) inc += nib_match(a.dir_prev[v - g.plane], 5);
-            if (m & 4u) inc += nib_match(a.dir_prev[v - g.gx], 3);
-            if (m & 1u) inc += nib_match(a.dir_prev[v - 1u], 1);
-            if (m & 2u) inc += nib_match(a.dir_prev[v + 1u], 0);
-            if (m & 8u) inc += nib_match(a.dir_prev[v + g.gx], 2);
-            if (m & 32u) inc += nib_match(a.dir_prev[v + g.plane], 4);
+#pragma unroll
+            for (uint32_t k = 0; k < 6; ++k) inc += (m & slot_bit(k)) ? nib_match(d[k], slot_code(k)) : 0u;
             if (LINK) {
                 const uint32_t li = a.rev_off[v], nl = a.rev_off[v + 1] - li;
+                uint8_t lc[kLinkUnroll];
 #pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k) {
-                    const uint32_t t = k < nl ? a.ltag_prev[li + k] : 0xFFFFFFFFu;
-                    if ((t >> 2) == r - 1u) inc += t & 3u;
-                }
+                for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, 0u);
+#pragma unroll
+                for (uint32_t k = 0; k < kLinkUnroll; ++k)
+                    if (k < nl && lc[k]) {
+                        inc += lc[k];
+                        a.lcnt_prev[li + k] = 0;
+                    }
                 for (uint32_t k = kLinkUnroll; k < nl; ++k) {
-                    const uint32_t t = a.ltag_prev[li + k];
-                    if ((t >> 2) == r - 1u) inc += t & 3u;
+                    const uint8_t c = a.lcnt_prev[li + k];
+                    if (c) {
+                        inc += c;
+                        a.lcnt_prev[li + k] = 0;
+                    }
                 }
             }
             if (inc) {
@@ -293,11 +308,12 @@ __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
             a.dir_cur[v] = (uint8_t)(c0 | (c1 << 4));
             if (LINK) {
                 const uint32_t nl = (uint32_t)(c0 == kDirLink) + (uint32_t)(c1 == kDirLink);
-                if (nl) a.ltag_cur[a.lpos[v]] = r * 4u + nl;
+                const uint32_t lp = load_sel(a.lpos, nl != 0u, v, 0u);
+                if (nl) a.lcnt_cur[lp] = (uint8_t)nl;
             }
         }
     }
-    if (r) block_add(newly, &a.total[r - 1]);
+    if (r) block_add(newly, a.parts, (long long)r - 1);
 }
 
 // ------------------------------------------------------------------ generic (bucketed) paths
@@ -319,7 +335,7 @@ __device__ __forceinline__ uint32_t generic_target(const RoundArgs& a, uint32_t 
 // Gossip on any topology (used for "full"): receipts are integer atomics into inc_cur[t]
 // (order-free, so exact); the done filter of program.fs:92 is applied receiver-side.
 __global__ __launch_bounds__(kBlock) void k_gs_push(RoundArgs a) {
-    if (gs_gate(a)) return;
+    if (a.r && gate(a, (long long)a.r - 1)) return;
     const uint32_t r = a.r;
     uint32_t v, end, step;
     node_range(a.g.actors, a.span, v, end, step);
@@ -353,7 +369,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_push(RoundArgs a) {
             if (tok > 1) atomicAdd(&a.inc_cur[generic_target(a, v, m, scale_draw(x.y, d))], 1u);
         }
     }
-    if (r) block_add(newly, &a.total[r - 1]);
+    if (r) block_add(newly, a.parts, (long long)r - 1);
 }
 
 // Push-sum on any topology (used for "full"): messages are bucketed by destination with an
@@ -361,7 +377,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_push(RoundArgs a) {
 // source order (selection by repeated minimum; buckets hold ~1 entry), so the fp64 sum is the
 // canonical one.
 __global__ __launch_bounds__(kBlock) void k_ps_push_emit(RoundArgs a) {
-    if (ps_gate(a)) return;
+    if (gate(a, a.r)) return;
     const uint32_t r = a.r;
     uint32_t v, end, step;
     node_range(a.g.actors, a.span, v, end, step);
@@ -411,11 +427,12 @@ __global__ __launch_bounds__(kBlock) void k_ps_push_emit(RoundArgs a) {
             ++newly;
         }
     }
-    block_add(newly, &a.total[r]);
+    block_add(newly, a.parts, r);
 }
 
 __global__ __launch_bounds__(kBlock) void k_ps_push_fill(RoundArgs a, uint32_t* slot_cur, const uint32_t* boff_cur) {
-    const unsigned long long prev = a.r ? a.total[a.r - 1] : 0ull;
+    unsigned long long prev = 0;  // completion after round r-1 (published by this round's emit)
+    if (a.r) prev = a.total[a.r - 1];
     if (prev >= a.target) return;
     uint32_t v, end, step;
     node_range(a.g.actors, a.span, v, end, step);
@@ -541,6 +558,18 @@ __global__ void k_fill_u8(uint8_t* p, uint8_t val, size_t n) {
         p[i] = val;
 }
 
+__global__ void k_fill_empty(double2* p, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        p[i] = make_double2(0.0, __longlong_as_double((long long)kEmptySlot));
+}
+
+__global__ void k_finalize(unsigned long long* total, uint32_t* parts, long long a) {
+    unsigned long long x = *part_slot(parts, a, threadIdx.x);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    if (threadIdx.x == 0) total[a] = x + (a >= 1 ? total[a - 1] : 0ull);
+}
+
 __global__ void k_ps_init(uint8_t* flags, Geom g, uint32_t full, uint32_t term_init) {
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < g.actors; v += gridDim.x * blockDim.x) {
         const bool part = full ? true : presence(g, v) != 0u;
@@ -656,6 +685,17 @@ void launch_fill_u8(uint8_t* p, uint8_t v, size_t n, hipStream_t s) {
     if (blocks > (size_t)kMaxGrid) blocks = kMaxGrid;
     if (blocks == 0) return;
     hipLaunchKernelGGL(k_fill_u8, dim3((unsigned)blocks), dim3(kBlock), 0, s, p, v, n);
+}
+
+void launch_fill_empty_slots(double2* p, size_t n, hipStream_t s) {
+    size_t blocks = (n + kBlock - 1) / kBlock;
+    if (blocks > (size_t)kMaxGrid) blocks = kMaxGrid;
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(k_fill_empty, dim3((unsigned)blocks), dim3(kBlock), 0, s, p, n);
+}
+
+void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, total, parts, a);
 }
 
 void launch_ps_init(uint8_t* flags, const Geom& g, uint32_t full, uint32_t term_init, const Launch& l) {
