@@ -135,7 +135,7 @@ struct Handle {
     template <class T>
     int alloc(T** p, size_t count) {
         void* q = nullptr;
-        const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+        const size_t bytes = count * sizeof(T) + 64;  // padding: vectorised tail reads stay in bounds
         hipError_t e = hipMalloc(&q, bytes);
         if (e != hipSuccess) return fail(GP_ENOMEM, "hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
         allocs.push_back(q);
@@ -309,41 +309,59 @@ const char* round_kernel_name(const Handle* h) {
     return h->generic ? "k_ps_push_emit" : (h->g.has_link ? "k_ps_pull<true>" : "k_ps_pull<false>");
 }
 
-// Algorithmic (compulsory) HBM bytes of one round kernel; DESIGN.md §5.
-//   push-sum pull: held (S,W) read 16 + message write 16 + direction byte write 1 + own
-//   direction/flag bytes read 2 per participant; Imp3D adds the link CSR (rev_off 4 per actor,
-//   source id 4 + slot 16 per link) and the pushed link message (16 per sender choosing it).
+// Compulsory HBM bytes of one launch of the dominant round kernel for its data layout
+// (every array element it must touch, touched once); DESIGN.md §5.
+//   push-sum pull: held (S,W) read 16 + message write 16 + flags read 1 + direction byte read
+//   1 (own row; neighbour rows re-read from cache) + direction write 1 per participant; Imp3D
+//   adds the link CSR offsets (4 per actor) and per link slot the 16-byte slot + 4-byte source.
+//   The link scatter pass (a separate kernel) is not included.
+//   gossip pull: state byte read 1 + direction byte read 1 + write 1 (+ count r/w 8 on the
+//   receipts, not modelled); Imp3D adds offsets 4 per actor and 1 per link slot.
 double bytes_per_round(const Handle* h) {
     const double P = (double)h->lay.participants, A = (double)h->lay.actors, links = (double)h->lay.links;
     if (h->gossip) {
         if (h->generic) return P * (4 + 4 + 1 + 1) + P * 2 * 4;  // cnt r/w, inc r, state r/w, 2 atomics
-        return P * (1 + 1 + 1) + (h->g.has_link ? 4 * A + 1 * links : 0);  // state r, dir r, dir w
+        return P * (1 + 1 + 1) + (h->g.has_link ? 4 * A + 1 * links : 0);
     }
     if (h->generic) return P * (16 + 16 + 16 + 1 + 4 + 4 + 4 + 4 + 4);
-    double b = P * (16 + 16 + 1 + 2);
-    if (h->g.has_link) b += 4 * A + links * (4 + 16) + 16.0 * links / 7.0;
+    double b = P * (16 + 16 + 1 + 1 + 1);
+    if (h->g.has_link) b += 4 * A + links * (16 + 4);
     return b;
 }
 
-int launch_round(Handle* h, int64_t k) {
+// The dominant round kernel F(k) (timed under GP_FLAG_KERNEL_TIMING) ...
+void launch_main(Handle* h, int64_t k) {
+    const RoundArgs a = h->args((uint32_t)k);
+    const Launch l = h->L();
+    if (h->gossip) {
+        if (h->generic) launch_gs_push(a, l);  // adds into inc_cur, consumed (zeroed) by F(k+1)
+        else launch_gs_pull(a, l);
+    } else if (h->generic) {
+        launch_ps_push_emit(a, l);
+    } else {
+        launch_ps_pull(a, l);
+    }
+}
+
+// ... and the passes that complete round k after it (link scatter; bucket scan + fill).
+void launch_aux(Handle* h, int64_t k) {
     const uint32_t r = (uint32_t)k;
     const RoundArgs a = h->args(r);
     const Launch l = h->L();
     if (h->gossip) {
-        if (h->generic) {
-            // F(r) adds into inc_cur, whose entries were consumed (zeroed) by F(r-1)
-            launch_gs_push(a, l);
-        } else {
-            launch_gs_pull(a, l);
-        }
+        if (!h->generic && h->g.has_link) launch_gs_link_scatter(a, l);
     } else if (h->generic) {
         const int c = (int)(r & 1u);
-        launch_ps_push_emit(a, l);
         launch_exclusive_scan(h->bcnt[c], h->boff[c], h->g.actors, h->scan_scratch, h->stream);
         launch_ps_push_fill(a, h->slot[c], h->boff[c], l);
-    } else {
-        launch_ps_pull(a, l);
+    } else if (h->g.has_link) {
+        launch_ps_link_scatter(a, l);
     }
+}
+
+int launch_round(Handle* h, int64_t k) {
+    launch_main(h, k);
+    launch_aux(h, k);
     return GP_OK;
 }
 
@@ -367,8 +385,9 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         }
         for (int64_t i = 0; i < B; ++i) {
             if (timing) HIP_TRY(hipEventRecord(h->kev[2 * i], h->stream));
-            if ((rc = launch_round(h, h->next_kernel + i))) return rc;
+            launch_main(h, h->next_kernel + i);
             if (timing) HIP_TRY(hipEventRecord(h->kev[2 * i + 1], h->stream));
+            launch_aux(h, h->next_kernel + i);
         }
         h->next_kernel += B;
         // total[] of the last round this batch applied (F(k) applies round k, or k-1 for gossip)

@@ -73,6 +73,8 @@ uint32_t span_for(uint32_t n, int grid);
 // round kernels
 void launch_ps_pull(const RoundArgs& a, const Launch& l);
 void launch_gs_pull(const RoundArgs& a, const Launch& l);
+void launch_ps_link_scatter(const RoundArgs& a, const Launch& l);
+void launch_gs_link_scatter(const RoundArgs& a, const Launch& l);
 void launch_ps_push_emit(const RoundArgs& a, const Launch& l);
 void launch_ps_push_fill(const RoundArgs& a, uint32_t* slot_cur, const uint32_t* boff_cur, const Launch& l);
 void launch_gs_push(const RoundArgs& a, const Launch& l);

@@ -158,13 +158,10 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
     for (; v < end; v += step) {
         const uint32_t m = presence(g, v);
         if (!m) continue;  // non-participant: never sends, never receives
-        // the draw is independent of state: do it first so lpos can be fetched early
         const uint32_t code = (a.ablate & 8u) ? kth_bit(m, v % popc(m))
                                               : kth_bit(m, scale_draw(philox(v, r, kStreamPush, a.seed).x, popc(m)));
         // ---- level 1
         uint8_t f = a.flags[v];
-        uint32_t lp = 0;
-        if (LINK) lp = load_sel(a.lpos, code == kDirLink, v, 0u);
         double2 held = make_double2((double)v, 1.0);  // InitializeVariables (program.fs:107-108)
         double ss = 0.0, ww = 0.0;  // inbox sum from +0.0 in ascending source order
         uint32_t cin = 0;
@@ -182,23 +179,40 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
 #pragma unroll
             for (uint32_t k = 0; k < 6; ++k) hits |= ((m & slot_bit(k)) && d[k] == slot_code(k)) ? 1u << k : 0u;
             if (a.ablate & 16u) hits = 0;
-            // ---- level 2
-            double2 gm[6];
+            // ---- level 2: the first three grid hits (Binomial(6, ~1/7): >99% of actors), in
+            // slot (= ascending source) order; more hits are picked up by the tail in flush()
+            uint32_t hk[3], rest = hits;
 #pragma unroll
-            for (uint32_t k = 0; k < 6; ++k) gm[k] = load_sel(a.msg_prev, (hits >> k) & 1u, slot_src(g, v, k), v);
+            for (int j = 0; j < 3; ++j) {
+                hk[j] = rest ? (uint32_t)__builtin_ctz(rest) : 6u;
+                rest &= rest - 1u;
+            }
+            double2 gm[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) gm[j] = load_sel(a.msg_prev, hk[j] < 6u, slot_src(g, v, hk[j] < 6u ? hk[j] : 0u), v);
+            uint32_t gi = 0;  // next grid hit to add (index into hk; >= 3 means the tail)
             auto add = [&](double2 mm) {
                 ss += mm.x;
                 ww += mm.y;
                 ++cin;
             };
-            // add pending grid messages from sources below `bound` (slots are ascending)
+            // add pending grid messages from sources below `bound` (hits are ascending)
             auto flush = [&](uint32_t bound) {
 #pragma unroll
-                for (uint32_t k = 0; k < 6; ++k)
-                    if ((hits & (1u << k)) && slot_src(g, v, k) < bound) {
-                        add(gm[k]);
-                        hits &= ~(1u << k);
+                for (int j = 0; j < 3; ++j)
+                    if (gi == (uint32_t)j && hk[j] < 6u && slot_src(g, v, hk[j]) < bound) {
+                        add(gm[j]);
+                        ++gi;
                     }
+                if (gi >= 3) {  // rare: a 4th+ grid hit (loaded on demand)
+                    while (rest) {
+                        const uint32_t k = (uint32_t)__builtin_ctz(rest);
+                        const uint32_t u = slot_src(g, v, k);
+                        if (u >= bound) break;
+                        add(a.msg_prev[u]);
+                        rest &= rest - 1u;
+                    }
+                }
             };
             if (LINK) {
                 double2 lm[kLinkUnroll];
@@ -229,10 +243,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
         }
         const uint8_t f0 = f;
         const PsOut o = ps_update(f, held, ss, ww, cin, a.delta, a.term_limit);
-        if (o.send) {
-            a.msg_cur[v] = o.msg;
-            if (LINK && code == kDirLink && !(a.ablate & 4u)) a.lmsg_cur[lp] = o.msg;
-        }
+        if (o.send) a.msg_cur[v] = o.msg;  // a link message is scattered by k_ps_link_scatter
         a.dir_cur[v] = o.send ? (uint8_t)code : kDirNone;
         if (f != f0) a.flags[v] = f;
         if (o.conv_now) {
@@ -306,14 +317,57 @@ __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
             const uint32_t c0 = kth_bit(m, scale_draw(x.x, d));
             const uint32_t c1 = tok > 1 ? kth_bit(m, scale_draw(x.y, d)) : 15u;
             a.dir_cur[v] = (uint8_t)(c0 | (c1 << 4));
-            if (LINK) {
-                const uint32_t nl = (uint32_t)(c0 == kDirLink) + (uint32_t)(c1 == kDirLink);
-                const uint32_t lp = load_sel(a.lpos, nl != 0u, v, 0u);
-                if (nl) a.lcnt_cur[lp] = (uint8_t)nl;
-            }
         }
     }
     if (r) block_add(newly, a.parts, (long long)r - 1);
+}
+
+// ------------------------------------------------------------------ link scatter passes
+// After F(r): every actor whose round-r message took its extra link (direction code 6) writes
+// it into its CSR slot, where the receiver scans it in F(r+1).  A separate pass so the round
+// kernel's loads never wait behind scattered stores (vmcnt counts stores on CDNA).
+// Four actors per thread (block-strided, so every load instruction stays coalesced): their
+// direction codes, then every link message's slot index and payload in flight together
+// (memory-level parallelism), then the scattered stores.
+constexpr uint32_t kScatterPer = 4;
+
+__global__ __launch_bounds__(kBlock) void k_ps_link_scatter(RoundArgs a) {
+    const uint32_t n = a.g.wired;
+    const uint32_t base = blockIdx.x * kBlock * kScatterPer + threadIdx.x;
+    bool l[kScatterPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j) {
+        const uint32_t u = base + j * kBlock;
+        l[j] = u < n && load_sel(a.dir_cur, u < n, u, 0u) == kDirLink;
+    }
+    uint32_t lp[kScatterPer];
+    double2 mm[kScatterPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j) {
+        const uint32_t u = base + j * kBlock;
+        lp[j] = load_sel(a.lpos, l[j], u, 0u);
+        mm[j] = load_sel(a.msg_cur, l[j], u, 0u);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j)
+        if (l[j] && !(a.ablate & 4u)) a.lmsg_cur[lp[j]] = mm[j];
+}
+
+__global__ __launch_bounds__(kBlock) void k_gs_link_scatter(RoundArgs a) {
+    const uint32_t n = a.g.wired;
+    const uint32_t base = blockIdx.x * kBlock * kScatterPer + threadIdx.x;
+    uint32_t nl[kScatterPer], lp[kScatterPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j) {
+        const uint32_t u = base + j * kBlock;
+        const uint8_t b = load_sel(a.dir_cur, u < n, u, 0u);
+        nl[j] = u < n ? (uint32_t)((b & 15u) == kDirLink) + (uint32_t)((b >> 4) == kDirLink) : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j) lp[j] = load_sel(a.lpos, nl[j] != 0u, base + j * kBlock, 0u);
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j)
+        if (nl[j]) a.lcnt_cur[lp[j]] = (uint8_t)nl[j];
 }
 
 // ------------------------------------------------------------------ generic (bucketed) paths
@@ -635,6 +689,16 @@ void launch_ps_pull(const RoundArgs& a, const Launch& l) {
 void launch_gs_pull(const RoundArgs& a, const Launch& l) {
     if (a.g.has_link) hipLaunchKernelGGL(k_gs_pull<true>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
     else hipLaunchKernelGGL(k_gs_pull<false>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+}
+
+// Flat grids (one actor per thread): a grid-stride loop would make each iteration's load wait
+// behind the previous iteration's scattered store.
+void launch_ps_link_scatter(const RoundArgs& a, const Launch& l) {
+    hipLaunchKernelGGL(k_ps_link_scatter, dim3((a.g.wired + kScatterPer * kBlock - 1) / (kScatterPer * kBlock)), dim3(kBlock), 0, l.stream, a);
+}
+
+void launch_gs_link_scatter(const RoundArgs& a, const Launch& l) {
+    hipLaunchKernelGGL(k_gs_link_scatter, dim3((a.g.wired + kScatterPer * kBlock - 1) / (kScatterPer * kBlock)), dim3(kBlock), 0, l.stream, a);
 }
 
 void launch_ps_push_emit(const RoundArgs& a, const Launch& l) {

@@ -1,0 +1,61 @@
+"""Turn rocprofv3 --pmc passes into profiles/<round>/pmc_summary.json and profiles/pmc_traffic.json.
+
+FETCH_SIZE/WRITE_SIZE are in KB per dispatch.  On gfx950 FETCH_SIZE under-reports wide
+coalesced reads by 2x (MI355X_MICROARCH.md §HBM); the factor actually applied is measured on
+tools/microbench/membench's copy kernel (known 159 MB read) and stored as fetch_correction.
+
+    python3 tools/make_pmc_traffic.py 'gpurun_out/r1/pmc_*' profiles/round1 "10000000 Imp3D push-sum" 'gpurun_out/r1/calib_*'
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+from collections import defaultdict
+
+src, dst, workload = sys.argv[1], sys.argv[2], sys.argv[3]
+calib = sys.argv[4] if len(sys.argv) > 4 else None
+
+
+def medians(root, skip_first=1):
+    """root: a directory or a glob of directories holding rocprofv3 counter_collection CSVs."""
+    agg = defaultdict(list)
+    files = [f for d in glob.glob(root) for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)]
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
+            agg[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
+    return {f"{k}|{c}": statistics.median(v[skip_first:] or v) for (k, c), v in agg.items()}
+
+
+m = medians(src)
+corr = 2.0
+calib_info = None
+if calib:
+    cm = medians(calib, skip_first=0)
+    fetch = [v for k, v in cm.items() if "copy_flat" in k and k.endswith("FETCH_SIZE")]
+    if fetch:
+        known = 9938376 * 16 / 1024.0  # KB read by copy_flat
+        corr = known / fetch[0]
+        calib_info = {"kernel": "membench copy_flat (16 B/lane coalesced read)", "fetch_kb": fetch[0],
+                      "known_kb": known, "factor": corr}
+out = {"workload": workload, "fetch_correction": corr, "calibration": calib_info, "medians": m}
+os.makedirs(dst, exist_ok=True)
+with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
+    json.dump(out, f, indent=1, sort_keys=True)
+traffic = {}
+for key, fetch in m.items():
+    k, c = key.split("|")
+    if c != "FETCH_SIZE":
+        continue
+    w = m.get(f"{k}|WRITE_SIZE")
+    if w is None:
+        continue
+    short = k.split("::")[-1]
+    traffic[short] = {"workload": workload, "fetch_kb": fetch, "write_kb": w, "fetch_correction": corr,
+                      "hbm_bytes_per_launch": (fetch * corr + w) * 1024.0,
+                      "source": os.path.join(dst, "pmc_summary.json")}
+with open(os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_traffic.json"), "w") as f:
+    json.dump(traffic, f, indent=1, sort_keys=True)
+print(json.dumps(traffic, indent=1))
