@@ -69,11 +69,37 @@ int sizes(int64_t n_arg, int32_t topology, int64_t* nodes, int64_t* actors, int6
     return GP_OK;
 }
 
+// Layout of one exchange chunk (peer p -> peer q); both ends compute it identically.
+struct Chunk {
+    size_t hdir = 0, hmsg = 0, slot = 0, msg = 0, size = 0;  // byte offsets / total size
+    uint32_t halo = 0;  // halo actors carried (0: none)
+    uint32_t cap = 0;   // link / receipt entries
+};
+
+constexpr size_t kAlign = 256;
+size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
 struct Handle {
     gp_config cfg{};
     gp_layout lay{};
     Geom g{};
     bool full = false, generic = false, gossip = false;
+    // node-range shard (whole graph: lo = 0, hi = actors, world = 1)
+    bool sharded = false;
+    int32_t rank = 0, world = 1;
+    uint32_t lo = 0, hi = 0;
+    uint32_t halo = 0;  // z-plane (Imp3D/3D) or 1 actor (line/2D) exchanged with rank +-1
+    std::vector<int64_t> abnd, sbnd;          // actor / link-slot bounds of every rank
+    std::vector<unsigned long long> lhist;    // (src rank, dst rank, degree) link counts
+    std::vector<Chunk> out_chunk, in_chunk;   // per peer
+    std::vector<int64_t> out_off, in_off;     // chunk offsets inside the send / recv buffers
+    int64_t send_total = 0, recv_total = 0;
+    uint32_t max_in_cap = 0;
+    uint32_t* pcount = nullptr;
+    uint32_t* overflow = nullptr;
+    unsigned long long* self_newly = nullptr;
+    void* pending_send = nullptr;  // gp_shard_round issued, gp_shard_deliver not yet
+    bool awaiting_deliver = false;
     hipStream_t stream = nullptr;
     bool own_stream = false;
     int grid = 0;
@@ -117,10 +143,12 @@ struct Handle {
     int64_t batch = 8;
     uint32_t ablate = 0;  // DEBUG: GP_ABLATE env var (cost attribution only; breaks results)
     // timing
-    std::vector<hipEvent_t> kev;
+    std::vector<hipEvent_t> kev;  // 3 per round: before main, after main, after aux
     hipEvent_t ev_a = nullptr, ev_b = nullptr;
     int64_t k_launches = 0;
-    double k_total_ms = 0.0;
+    double k_total_ms = 0.0, k_aux_ms = 0.0;
+    int64_t timed_first = 0;  // sharded: round index of kev[0..2]
+    int64_t timed_count = 0;
 
     ~Handle() {
         if (stream) (void)hipStreamSynchronize(stream);
@@ -132,17 +160,24 @@ struct Handle {
         if (own_stream && stream) (void)hipStreamDestroy(stream);
     }
 
+    // Device array holding elements [first, first + count) of a global index space; *p is
+    // biased by -first so kernels index it with global actor / slot ids.
     template <class T>
-    int alloc(T** p, size_t count) {
+    int alloc(T** p, size_t count, int64_t first = 0) {
         void* q = nullptr;
         const size_t bytes = count * sizeof(T) + 64;  // padding: vectorised tail reads stay in bounds
         hipError_t e = hipMalloc(&q, bytes);
         if (e != hipSuccess) return fail(GP_ENOMEM, "hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
         allocs.push_back(q);
         dev_bytes += bytes;
-        *p = static_cast<T*>(q);
+        *p = reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(q) - (uintptr_t)first * sizeof(T));
         return GP_OK;
     }
+
+    // actors whose round-to-round messages this rank keeps: own range plus both halos
+    int64_t ext_lo() const { return std::max<int64_t>(0, (int64_t)lo - halo); }
+    int64_t ext_hi() const { return std::min<int64_t>(g.actors, (int64_t)hi + halo); }
+    uint32_t own() const { return hi - lo; }
 
     Launch L() const { return Launch{grid, stream}; }
 
@@ -150,6 +185,10 @@ struct Handle {
         RoundArgs a{};
         a.g = g;
         a.seed = cfg.seed;
+        a.lo = lo;
+        a.hi = hi;
+        a.slot_lo = sbnd.empty() ? 0u : (uint32_t)sbnd[rank];
+        a.sharded = sharded ? 1u : 0u;
         a.r = r;
         a.target = (uint32_t)lay.nodes;
         a.full = full ? 1u : 0u;
@@ -192,20 +231,19 @@ struct Handle {
 
 Handle* H(void* h) { return static_cast<Handle*>(h); }
 
+Xchg base_xchg(const Handle* h);
+
+// Imp3D extra links (program.fs:309) and their receiver-side CSR, for the whole graph: each
+// rank draws every link itself (Philox is global), so no exchange is needed to learn which
+// remote senders target its actors or at which CSR slot.  A shard keeps link slots for its
+// own destinations only.
 int build_links(Handle* h) {
     const uint32_t nodes = (uint32_t)h->lay.nodes, A = h->g.actors;
     int rc;
     if ((rc = h->alloc(&h->link, nodes))) return rc;
     if ((rc = h->alloc(&h->rev_off, (size_t)A + 1))) return rc;
     if ((rc = h->alloc(&h->rev_src, nodes))) return rc;
-    if (!h->generic) {  // pull kernels: sender-pushed link slots
-        if ((rc = h->alloc(&h->lpos, nodes))) return rc;
-        if (h->gossip) {
-            if ((rc = h->alloc(&h->lcnt[0], nodes)) || (rc = h->alloc(&h->lcnt[1], nodes))) return rc;
-        } else if ((rc = h->alloc(&h->lmsg[0], nodes)) || (rc = h->alloc(&h->lmsg[1], nodes))) {
-            return rc;
-        }
-    }
+    if (!h->generic && (rc = h->alloc(&h->lpos, nodes))) return rc;
     uint32_t *counts = nullptr, *scratch = nullptr;
     HIP_TRY(hipMalloc(&counts, ((size_t)A + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&scratch, scan_scratch_words(A) * sizeof(uint32_t)));
@@ -229,6 +267,35 @@ int build_links(Handle* h) {
     (void)hipFree(scratch);
     if (e != hipSuccess) return fail(GP_EHIP, "extra-link CSR build failed: %s", hipGetErrorString(e));
     h->lay.links = nodes;
+    // link-slot range of every rank (contiguous: destinations are)
+    h->sbnd.assign((size_t)h->world + 1, 0);
+    for (int q = 0; q <= h->world; ++q) {
+        uint32_t v = 0;
+        HIP_TRY(hipMemcpy(&v, h->rev_off + h->abnd[q], sizeof v, hipMemcpyDeviceToHost));
+        h->sbnd[q] = v;
+    }
+    const int64_t slo = h->sbnd[h->rank], nsl = h->sbnd[h->rank + 1] - slo;
+    if (!h->generic) {  // pull kernels: sender-pushed link slots
+        if (h->gossip) {
+            if ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))) return rc;
+        } else if ((rc = h->alloc(&h->lmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lmsg[1], (size_t)nsl, slo))) {
+            return rc;
+        }
+    }
+    if (h->sharded) {  // link counts per (source rank, destination rank, sender degree)
+        const size_t nb = (size_t)h->world * h->world * 8;
+        unsigned long long* hist = nullptr;
+        HIP_TRY(hipMalloc(&hist, nb * sizeof *hist));
+        e = hipMemsetAsync(hist, 0, nb * sizeof *hist, h->stream);
+        if (e == hipSuccess) {
+            launch_link_hist(h->link, h->g, base_xchg(h), hist, l);
+            h->lhist.assign(nb, 0);
+            e = hipMemcpyAsync(h->lhist.data(), hist, nb * sizeof *hist, hipMemcpyDeviceToHost, h->stream);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        (void)hipFree(hist);
+        if (e != hipSuccess) return fail(GP_EHIP, "link histogram failed: %s", hipGetErrorString(e));
+    }
     return GP_OK;
 }
 
@@ -257,41 +324,51 @@ int ensure_trace(Handle* h, int64_t need) {
 
 int reset(Handle* h) {
     HIP_TRY(hipStreamSynchronize(h->stream));
-    const size_t A = h->g.actors;
+    const size_t lo = h->lo, n = h->own();
+    const size_t xlo = (size_t)h->ext_lo(), xn = (size_t)(h->ext_hi() - h->ext_lo());
     HIP_TRY(hipMemsetAsync(h->total, 0, (size_t)h->total_cap * sizeof(unsigned long long), h->stream));
     HIP_TRY(hipMemsetAsync(h->parts, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t), h->stream));
-    for (int i = 0; i < 2; ++i) {  // no link message in flight
-        if (h->lcnt[i]) HIP_TRY(hipMemsetAsync(h->lcnt[i], 0, (size_t)h->lay.nodes, h->stream));
-        if (h->lmsg[i]) launch_fill_empty_slots(h->lmsg[i], (size_t)h->lay.nodes, h->stream);
+    if (h->sharded) {
+        HIP_TRY(hipMemsetAsync(h->pcount, 0, (size_t)h->world * sizeof(uint32_t), h->stream));
+        HIP_TRY(hipMemsetAsync(h->overflow, 0, sizeof(uint32_t), h->stream));
+    }
+    if (h->lcnt[0] || h->lmsg[0]) {  // no link message in flight
+        const size_t slo = (size_t)h->sbnd[h->rank], ns = (size_t)(h->sbnd[h->rank + 1] - h->sbnd[h->rank]);
+        for (int i = 0; i < 2; ++i) {
+            if (h->lcnt[i]) HIP_TRY(hipMemsetAsync(h->lcnt[i] + slo, 0, ns, h->stream));
+            if (h->lmsg[i]) launch_fill_empty_slots(h->lmsg[i] + slo, ns, h->stream);
+        }
     }
     if (!h->gossip) {
-        launch_ps_init(h->flags, h->g, h->full ? 1u : 0u, (uint32_t)h->cfg.term_init, h->L());
+        launch_ps_init(h->flags, h->g, h->lo, h->hi, h->full ? 1u : 0u, (uint32_t)h->cfg.term_init, h->L());
         if (h->generic) {
-            HIP_TRY(hipMemsetAsync(h->bcnt[0], 0, A * sizeof(uint32_t), h->stream));
-            HIP_TRY(hipMemsetAsync(h->bcnt[1], 0, A * sizeof(uint32_t), h->stream));
-            HIP_TRY(hipMemsetAsync(h->tgt, 0xFF, A * sizeof(uint32_t), h->stream));
+            HIP_TRY(hipMemsetAsync(h->bcnt[0] + lo, 0, n * sizeof(uint32_t), h->stream));
+            HIP_TRY(hipMemsetAsync(h->bcnt[1] + lo, 0, n * sizeof(uint32_t), h->stream));
+            HIP_TRY(hipMemsetAsync(h->tgt + lo, 0xFF, n * sizeof(uint32_t), h->stream));
         } else {
-            launch_fill_u8(h->dir[0], kDirNone, A, h->stream);
-            launch_fill_u8(h->dir[1], kDirNone, A, h->stream);
+            launch_fill_u8(h->dir[0] + xlo, kDirNone, xn, h->stream);
+            launch_fill_u8(h->dir[1] + xlo, kDirNone, xn, h->stream);
         }
     } else {
-        HIP_TRY(hipMemsetAsync(h->cnt, 0, A * sizeof(uint32_t), h->stream));
-        HIP_TRY(hipMemsetAsync(h->gstate, 0, A, h->stream));
+        HIP_TRY(hipMemsetAsync(h->cnt + lo, 0, n * sizeof(uint32_t), h->stream));
+        HIP_TRY(hipMemsetAsync(h->gstate + lo, 0, n, h->stream));
         if (h->generic) {
-            HIP_TRY(hipMemsetAsync(h->inc[0], 0, A * sizeof(uint32_t), h->stream));
-            HIP_TRY(hipMemsetAsync(h->inc[1], 0, A * sizeof(uint32_t), h->stream));
+            HIP_TRY(hipMemsetAsync(h->inc[0] + lo, 0, n * sizeof(uint32_t), h->stream));
+            HIP_TRY(hipMemsetAsync(h->inc[1] + lo, 0, n * sizeof(uint32_t), h->stream));
         } else {
-            launch_fill_u8(h->dir[0], 0xFF, A, h->stream);
-            launch_fill_u8(h->dir[1], 0xFF, A, h->stream);
+            launch_fill_u8(h->dir[0] + xlo, 0xFF, xn, h->stream);
+            launch_fill_u8(h->dir[1] + xlo, 0xFF, xn, h->stream);
         }
         // kick-off (program.fs:181/218/258/323): the leader holds one activation chain; for
         // "full" it is a CallChildActor, i.e. also its first receipt.
         const uint32_t L = (uint32_t)h->lay.leader;
-        const uint8_t st = 1;
-        HIP_TRY(hipMemcpyAsync(h->gstate + L, &st, 1, hipMemcpyHostToDevice, h->stream));
-        if (h->full) {
-            const uint32_t one = 1;
-            HIP_TRY(hipMemcpyAsync(h->cnt + L, &one, sizeof one, hipMemcpyHostToDevice, h->stream));
+        if (L >= h->lo && L < h->hi) {
+            const uint8_t st = 1;
+            HIP_TRY(hipMemcpyAsync(h->gstate + L, &st, 1, hipMemcpyHostToDevice, h->stream));
+            if (h->full) {
+                const uint32_t one = 1;
+                HIP_TRY(hipMemcpyAsync(h->cnt + L, &one, sizeof one, hipMemcpyHostToDevice, h->stream));
+            }
         }
     }
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -301,12 +378,20 @@ int reset(Handle* h) {
     h->completed = 0;
     h->converged = false;
     h->batch = 8;
+    h->awaiting_deliver = false;
+    h->timed_count = 0;
     return GP_OK;
 }
 
 const char* round_kernel_name(const Handle* h) {
     if (h->gossip) return h->generic ? "k_gs_push" : (h->g.has_link ? "k_gs_pull<true>" : "k_gs_pull<false>");
     return h->generic ? "k_ps_push_emit" : (h->g.has_link ? "k_ps_pull<true>" : "k_ps_pull<false>");
+}
+
+const char* aux_kernel_name(const Handle* h) {
+    if (h->generic) return h->gossip ? "" : "k_scan_* + k_ps_push_fill";
+    if (!h->g.has_link) return "";
+    return h->gossip ? "k_gs_link_scatter" : "k_ps_link_scatter";
 }
 
 // Compulsory HBM bytes of one launch of the dominant round kernel for its data layout
@@ -318,7 +403,8 @@ const char* round_kernel_name(const Handle* h) {
 //   gossip pull: state byte read 1 + direction byte read 1 + write 1 (+ count r/w 8 on the
 //   receipts, not modelled); Imp3D adds offsets 4 per actor and 1 per link slot.
 double bytes_per_round(const Handle* h) {
-    const double P = (double)h->lay.participants, A = (double)h->lay.actors, links = (double)h->lay.links;
+    const double frac = (double)h->own() / (double)h->g.actors;  // a shard's share
+    const double P = (double)h->lay.participants * frac, A = (double)h->own(), links = (double)h->lay.links * frac;
     if (h->gossip) {
         if (h->generic) return P * (4 + 4 + 1 + 1) + P * 2 * 4;  // cnt r/w, inc r, state r/w, 2 atomics
         return P * (1 + 1 + 1) + (h->g.has_link ? 4 * A + 1 * links : 0);
@@ -330,12 +416,16 @@ double bytes_per_round(const Handle* h) {
 }
 
 // The dominant round kernel F(k) (timed under GP_FLAG_KERNEL_TIMING) ...
-void launch_main(Handle* h, int64_t k) {
+void launch_main(Handle* h, int64_t k, const Xchg* x) {
     const RoundArgs a = h->args((uint32_t)k);
     const Launch l = h->L();
     if (h->gossip) {
-        if (h->generic) launch_gs_push(a, l);  // adds into inc_cur, consumed (zeroed) by F(k+1)
-        else launch_gs_pull(a, l);
+        if (h->generic) {  // adds into inc_cur, consumed (zeroed) by F(k+1)
+            if (x) launch_gs_push_x(a, *x, l);
+            else launch_gs_push(a, l);
+        } else {
+            launch_gs_pull(a, l);
+        }
     } else if (h->generic) {
         launch_ps_push_emit(a, l);
     } else {
@@ -344,51 +434,90 @@ void launch_main(Handle* h, int64_t k) {
 }
 
 // ... and the passes that complete round k after it (link scatter; bucket scan + fill).
-void launch_aux(Handle* h, int64_t k) {
+void launch_aux(Handle* h, int64_t k, const Xchg* x) {
     const uint32_t r = (uint32_t)k;
     const RoundArgs a = h->args(r);
     const Launch l = h->L();
     if (h->gossip) {
-        if (!h->generic && h->g.has_link) launch_gs_link_scatter(a, l);
+        if (!h->generic && h->g.has_link) {
+            if (x) launch_gs_link_scatter_x(a, *x, l);
+            else launch_gs_link_scatter(a, l);
+        }
     } else if (h->generic) {
         const int c = (int)(r & 1u);
         launch_exclusive_scan(h->bcnt[c], h->boff[c], h->g.actors, h->scan_scratch, h->stream);
         launch_ps_push_fill(a, h->slot[c], h->boff[c], l);
     } else if (h->g.has_link) {
-        launch_ps_link_scatter(a, l);
+        if (x) launch_ps_link_scatter_x(a, *x, l);
+        else launch_ps_link_scatter(a, l);
     }
 }
 
-int launch_round(Handle* h, int64_t k) {
-    launch_main(h, k);
-    launch_aux(h, k);
+int ensure_events(Handle* h, int64_t rounds) {
+    const size_t need = (size_t)(3 * rounds);
+    if (h->kev.size() >= need) return GP_OK;
+    const size_t old = h->kev.size();
+    h->kev.resize(need);
+    for (size_t i = old; i < need; ++i) HIP_TRY(hipEventCreate(&h->kev[i]));
+    return GP_OK;
+}
+
+// Round k with its three timing events (slot i of the event ring).
+int launch_round(Handle* h, int64_t k, const Xchg* x, bool timing, int64_t i) {
+    if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i], h->stream));
+    launch_main(h, k, x);
+    if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i + 1], h->stream));
+    launch_aux(h, k, x);
+    if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i + 2], h->stream));
+    return GP_OK;
+}
+
+int accumulate_timing(Handle* h, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) {
+        float m = 0.f, x = 0.f;
+        HIP_TRY(hipEventElapsedTime(&m, h->kev[3 * i], h->kev[3 * i + 1]));
+        HIP_TRY(hipEventElapsedTime(&x, h->kev[3 * i + 1], h->kev[3 * i + 2]));
+        h->k_total_ms += m;
+        h->k_aux_ms += x;
+    }
+    h->k_launches += n;
+    return GP_OK;
+}
+
+int fill_sums(Handle* h, gp_status* st) {
+    if (h->gossip) return GP_OK;
+    const int64_t last = h->rounds - 1;
+    RoundArgs a = h->args((uint32_t)std::max<int64_t>(last, 0));
+    a.msg_prev = h->msg[last >= 0 ? (last & 1) : 0];
+    a.dir_prev = h->generic ? nullptr : h->dir[last >= 0 ? (last & 1) : 0];
+    launch_ps_sums(a, last >= 0 ? 1u : 0u, h->partials, h->L());
+    std::vector<double2> part((size_t)h->grid);
+    HIP_TRY(hipMemcpyAsync(part.data(), h->partials, part.size() * sizeof(double2), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    for (const double2& p : part) {
+        st->sum_s += p.x;
+        st->sum_w += p.y;
+    }
     return GP_OK;
 }
 
 int step(Handle* h, int64_t max_rounds, gp_status* st) {
     if (max_rounds < 0) return fail(GP_EINVAL, "max_rounds < 0");
+    if (h->sharded) return fail(GP_ESTATE, "a shard advances with gp_shard_round / gp_shard_deliver");
     const bool timing = (h->cfg.flags & GP_FLAG_KERNEL_TIMING) != 0;
     HIP_TRY(hipEventRecord(h->ev_a, h->stream));
     const int64_t goal = h->rounds + max_rounds;
+    int rc;
     while (!h->converged && h->rounds < goal) {
         const int64_t B = std::min<int64_t>(h->batch, goal - h->rounds);
-        int rc;
         if ((rc = ensure_trace(h, h->next_kernel + B + 4))) return rc;
         if (h->gossip && h->next_kernel == 0) {  // F(0) only emits round 0
-            if ((rc = launch_round(h, 0))) return rc;
+            if ((rc = launch_round(h, 0, nullptr, false, 0))) return rc;
             h->next_kernel = 1;
         }
-        if (timing && (int64_t)h->kev.size() < 2 * B) {
-            const size_t old = h->kev.size();
-            h->kev.resize((size_t)(2 * B));
-            for (size_t i = old; i < h->kev.size(); ++i) HIP_TRY(hipEventCreate(&h->kev[i]));
-        }
-        for (int64_t i = 0; i < B; ++i) {
-            if (timing) HIP_TRY(hipEventRecord(h->kev[2 * i], h->stream));
-            launch_main(h, h->next_kernel + i);
-            if (timing) HIP_TRY(hipEventRecord(h->kev[2 * i + 1], h->stream));
-            launch_aux(h, h->next_kernel + i);
-        }
+        if (timing && (rc = ensure_events(h, B))) return rc;
+        for (int64_t i = 0; i < B; ++i)
+            if ((rc = launch_round(h, h->next_kernel + i, nullptr, timing, i))) return rc;
         h->next_kernel += B;
         // total[] of the last round this batch applied (F(k) applies round k, or k-1 for gossip)
         launch_finalize(h->total, h->parts, h->next_kernel - (h->gossip ? 2 : 1), h->stream);
@@ -413,14 +542,7 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         }
         h->completed = (int64_t)h->h_trace[real - 1];
         h->rounds += real;
-        if (timing) {
-            for (int64_t i = 0; i < real; ++i) {
-                float ms = 0.f;
-                HIP_TRY(hipEventElapsedTime(&ms, h->kev[2 * i], h->kev[2 * i + 1]));
-                h->k_total_ms += ms;
-            }
-            h->k_launches += real;
-        }
+        if (timing && (rc = accumulate_timing(h, real))) return rc;
         h->batch = std::min<int64_t>(h->batch * 2, 256);
     }
     HIP_TRY(hipEventRecord(h->ev_b, h->stream));
@@ -433,28 +555,244 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         st->completed = h->completed;
         st->converged = h->converged ? 1 : 0;
         st->device_ms = ms;
-        if (!h->gossip) {
-            const int64_t last = h->rounds - 1;
-            RoundArgs a = h->args((uint32_t)std::max<int64_t>(last, 0));
-            a.msg_prev = h->msg[last >= 0 ? (last & 1) : 0];
-            a.dir_prev = h->generic ? nullptr : h->dir[last >= 0 ? (last & 1) : 0];
-            launch_ps_sums(a, last >= 0 ? 1u : 0u, h->partials, h->L());
-            std::vector<double2> part((size_t)h->grid);
-            HIP_TRY(hipMemcpyAsync(part.data(), h->partials, part.size() * sizeof(double2), hipMemcpyDeviceToHost,
-                                   h->stream));
-            HIP_TRY(hipStreamSynchronize(h->stream));
-            for (const double2& p : part) {
-                st->sum_s += p.x;
-                st->sum_w += p.y;
-            }
-        }
+        if ((rc = fill_sums(h, st))) return rc;
     }
     return GP_OK;
 }
 
+// ------------------------------------------------------------------ node-range shards
+int partition(int64_t n_arg, int32_t topology, int32_t world, std::vector<int64_t>& b) {
+    if (world < 1 || world > kMaxWorld) return fail(GP_EINVAL, "world %d outside 1..%d", world, kMaxWorld);
+    int64_t nodes, actors, grid;
+    int rc = sizes(n_arg, topology, &nodes, &actors, &grid);
+    if (rc) return rc;
+    b.assign((size_t)world + 1, 0);
+    if (topology == GP_IMP3D || topology == GP_THREE_D) {  // whole z-planes; the isolated actor goes last
+        const int64_t plane = grid * grid, planes = (nodes + plane - 1) / plane;
+        if (planes < world) return fail(GP_EINVAL, "%lld z-planes cannot be split over %d ranks", (long long)planes, world);
+        for (int q = 1; q < world; ++q) b[q] = (int64_t)q * planes / world * plane;
+    } else {
+        if (actors < 2LL * world) return fail(GP_EINVAL, "%lld actors cannot be split over %d ranks", (long long)actors, world);
+        for (int q = 1; q < world; ++q) b[q] = (int64_t)q * actors / world;
+    }
+    b[world] = actors;
+    return GP_OK;
+}
+
+// Entries per round from rank p to rank q, bounded: the exact maximum when small, otherwise the
+// mean + 8 sigma of its (binomial) distribution — an overflow is reported, never dropped.
+uint32_t entry_cap(double mean, double exact_max) {
+    const double c = std::ceil(mean + 8.0 * std::sqrt(mean) + 256.0);
+    return (uint32_t)std::min(c, exact_max);
+}
+
+Chunk chunk_layout(const Handle* h, int p, int q) {
+    Chunk c;
+    size_t off = kAlign;  // ShardHeader
+    const int64_t size_p = h->abnd[p + 1] - h->abnd[p];
+    if (h->halo && (q == p - 1 || q == p + 1)) {  // p's first (to p-1) or last (to p+1) actors
+        c.halo = (uint32_t)std::min<int64_t>(h->halo, size_p);
+        c.hdir = off;
+        off = align_up(off + c.halo);
+        if (!h->gossip) {
+            c.hmsg = off;
+            off = align_up(off + (size_t)c.halo * sizeof(double2));
+        }
+    }
+    double mean = 0.0, exact = 0.0;
+    if (h->full) {  // every chain of p draws a target uniform over the other actors
+        const double chains = 2.0 * (double)size_p, share = (double)(h->abnd[q + 1] - h->abnd[q]) / (double)h->lay.nodes;
+        mean = chains * share;
+        exact = chains;
+    } else if (h->g.has_link) {
+        for (int d = 1; d < 8; ++d) {
+            const double n = (double)h->lhist[((size_t)p * h->world + q) * 8 + d];
+            const double pick = h->gossip ? 1.0 - (1.0 - 1.0 / d) * (1.0 - 1.0 / d) : 1.0 / d;
+            mean += n * pick;
+            exact += n;
+        }
+    }
+    c.cap = entry_cap(mean, exact);
+    if (exact == 0.0) c.cap = 0;
+    c.slot = off;
+    off = align_up(off + (size_t)c.cap * sizeof(uint32_t));
+    if (!h->gossip) {
+        c.msg = off;
+        off = align_up(off + (size_t)c.cap * sizeof(double2));
+    }
+    c.size = off;
+    return c;
+}
+
+int build_plan(Handle* h) {
+    const int W = h->world, p = h->rank;
+    h->out_chunk.assign((size_t)W, Chunk{});
+    h->in_chunk.assign((size_t)W, Chunk{});
+    h->out_off.assign((size_t)W, 0);
+    h->in_off.assign((size_t)W, 0);
+    int64_t so = 0, ro = 0;
+    h->max_in_cap = 0;
+    for (int q = 0; q < W; ++q) {
+        if (q != p) {
+            h->out_chunk[q] = chunk_layout(h, p, q);
+            h->in_chunk[q] = chunk_layout(h, q, p);
+            h->max_in_cap = std::max(h->max_in_cap, h->in_chunk[q].cap);
+        }
+        h->out_off[q] = so;
+        h->in_off[q] = ro;
+        so += (int64_t)h->out_chunk[q].size;
+        ro += (int64_t)h->in_chunk[q].size;
+    }
+    h->send_total = so;
+    h->recv_total = ro;
+    int rc;
+    if ((rc = h->alloc(&h->pcount, (size_t)W)) || (rc = h->alloc(&h->overflow, 1)) || (rc = h->alloc(&h->self_newly, 1)))
+        return rc;
+    return GP_OK;
+}
+
+// Exchange descriptor with every device pointer except the buffers.
+Xchg base_xchg(const Handle* h) {
+    Xchg x{};
+    x.world = (uint32_t)h->world;
+    x.rank = (uint32_t)h->rank;
+    for (int q = 0; q <= h->world && q <= kMaxWorld; ++q) {
+        x.abnd[q] = (uint32_t)h->abnd[q];
+        x.sbnd[q] = q < (int)h->sbnd.size() ? (uint32_t)h->sbnd[q] : 0u;
+    }
+    x.pcount = h->pcount;
+    x.overflow = h->overflow;
+    x.self_newly = h->self_newly;
+    return x;
+}
+
+Xchg make_xchg(const Handle* h, void* send, const void* recv) {
+    Xchg x = base_xchg(h);
+    for (int q = 0; q < h->world; ++q) {
+        if (q == h->rank) continue;
+        if (send) {
+            char* b = static_cast<char*>(send) + h->out_off[q];
+            const Chunk& c = h->out_chunk[q];
+            x.out[q] = PeerOut{reinterpret_cast<ShardHeader*>(b), reinterpret_cast<uint32_t*>(b + c.slot),
+                               c.msg ? reinterpret_cast<double2*>(b + c.msg) : nullptr, c.cap};
+        }
+        if (recv) {
+            const char* b = static_cast<const char*>(recv) + h->in_off[q];
+            const Chunk& c = h->in_chunk[q];
+            x.in[q] = PeerIn{reinterpret_cast<const ShardHeader*>(b), reinterpret_cast<const uint32_t*>(b + c.slot),
+                             c.msg ? reinterpret_cast<const double2*>(b + c.msg) : nullptr, c.cap};
+        }
+    }
+    return x;
+}
+
+// Index of the round F(k) applies (its completion count), -1 for gossip's emit-only F(0).
+long long applied_round(const Handle* h, int64_t k) { return h->gossip ? (long long)k - 1 : (long long)k; }
+
+int shard_round(Handle* h, void* send) {
+    if (h->awaiting_deliver) return fail(GP_ESTATE, "gp_shard_deliver must follow gp_shard_round");
+    if (!send && h->send_total) return fail(GP_EINVAL, "null send buffer");
+    if (reinterpret_cast<uintptr_t>(send) % kAlign) return fail(GP_EINVAL, "send buffer not %zu-byte aligned", kAlign);
+    const bool timing = (h->cfg.flags & GP_FLAG_KERNEL_TIMING) != 0;
+    const int64_t k = h->next_kernel;
+    int rc;
+    if ((rc = ensure_trace(h, k + 4))) return rc;
+    if (timing && (rc = ensure_events(h, h->timed_count + 1))) return rc;
+    const Xchg x = make_xchg(h, send, nullptr);
+    if (timing && k >= (h->gossip ? 1 : 0)) {
+        if (h->timed_count == 0) h->timed_first = k;
+        if ((rc = launch_round(h, k, &x, true, h->timed_count))) return rc;
+        ++h->timed_count;
+    } else if ((rc = launch_round(h, k, &x, false, 0))) {
+        return rc;
+    }
+    const RoundArgs a = h->args((uint32_t)k);
+    launch_shard_pack(a, x, applied_round(h, k), h->stream);
+    // halo faces: this rank's first actors to rank-1, its last actors to rank+1
+    const int p = h->rank;
+    for (int q : {p - 1, p + 1}) {
+        if (q < 0 || q >= h->world || !h->out_chunk[q].halo) continue;
+        const Chunk& c = h->out_chunk[q];
+        const uint32_t first = q < p ? h->lo : h->hi - c.halo;
+        char* b = static_cast<char*>(send) + h->out_off[q];
+        HIP_TRY(hipMemcpyAsync(b + c.hdir, h->dir[k & 1] + first, c.halo, hipMemcpyDeviceToDevice, h->stream));
+        if (!h->gossip)
+            HIP_TRY(hipMemcpyAsync(b + c.hmsg, h->msg[k & 1] + first, (size_t)c.halo * sizeof(double2),
+                                   hipMemcpyDeviceToDevice, h->stream));
+    }
+    HIP_TRY(hipGetLastError());
+    h->awaiting_deliver = true;
+    h->pending_send = send;
+    return GP_OK;
+}
+
+int shard_deliver(Handle* h, const void* recv) {
+    if (!h->awaiting_deliver) return fail(GP_ESTATE, "gp_shard_deliver without gp_shard_round");
+    if (!recv && h->recv_total) return fail(GP_EINVAL, "null receive buffer");
+    if (reinterpret_cast<uintptr_t>(recv) % kAlign) return fail(GP_EINVAL, "receive buffer not %zu-byte aligned", kAlign);
+    const int64_t k = h->next_kernel;
+    const int p = h->rank;
+    for (int q : {p - 1, p + 1}) {  // rank-1's last actors sit below lo, rank+1's first at hi
+        if (q < 0 || q >= h->world || !h->in_chunk[q].halo) continue;
+        const Chunk& c = h->in_chunk[q];
+        const uint32_t first = q < p ? h->lo - c.halo : h->hi;
+        const char* b = static_cast<const char*>(recv) + h->in_off[q];
+        HIP_TRY(hipMemcpyAsync(h->dir[k & 1] + first, b + c.hdir, c.halo, hipMemcpyDeviceToDevice, h->stream));
+        if (!h->gossip)
+            HIP_TRY(hipMemcpyAsync(h->msg[k & 1] + first, b + c.hmsg, (size_t)c.halo * sizeof(double2),
+                                   hipMemcpyDeviceToDevice, h->stream));
+    }
+    const Xchg x = make_xchg(h, h->pending_send, recv);
+    launch_shard_unpack(h->args((uint32_t)k), x, applied_round(h, k), h->max_in_cap, h->gossip ? 1 : 0,
+                        h->full ? 1 : 0, h->stream);
+    HIP_TRY(hipGetLastError());
+    h->awaiting_deliver = false;
+    h->next_kernel = k + 1;
+    return GP_OK;
+}
+
+int shard_sync(Handle* h, gp_status* st) {
+    if (h->awaiting_deliver) return fail(GP_ESTATE, "gp_shard_sync between gp_shard_round and gp_shard_deliver");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    uint32_t of = 0;
+    HIP_TRY(hipMemcpy(&of, h->overflow, sizeof of, hipMemcpyDeviceToHost));
+    if (of & 2u) return fail(GP_EOVERFLOW, "a shard received an entry outside its range; the run is void");
+    if (of) return fail(GP_EOVERFLOW, "a shard exchange buffer overflowed; the run is void");
+    const int64_t applied = (int64_t)applied_round(h, h->next_kernel - 1) + 1;  // rounds whose counts exist
+    int64_t timed_real = h->timed_count;
+    if (!h->converged && applied > h->rounds) {
+        const int64_t n = applied - h->rounds;
+        std::vector<unsigned long long> t((size_t)n);
+        HIP_TRY(hipMemcpy(t.data(), h->total + h->rounds, (size_t)n * sizeof t[0], hipMemcpyDeviceToHost));
+        int64_t real = n;
+        for (int64_t i = 0; i < n; ++i)
+            if ((int64_t)t[i] >= h->lay.nodes) {
+                real = i + 1;
+                h->converged = true;
+                break;
+            }
+        h->completed = (int64_t)t[real - 1];
+        if (h->converged) timed_real = std::max<int64_t>(0, std::min<int64_t>(h->timed_count, h->rounds + real - h->timed_first + (h->gossip ? 1 : 0)));
+        h->rounds += real;
+    }
+    int rc;
+    if (h->timed_count && (rc = accumulate_timing(h, timed_real))) return rc;
+    h->timed_count = 0;
+    if (st) {
+        std::memset(st, 0, sizeof *st);
+        st->round = h->rounds;
+        st->completed = h->completed;
+        st->converged = h->converged ? 1 : 0;
+        if ((rc = fill_sums(h, st))) return rc;
+    }
+    return GP_OK;
+}
+
+// Read-back ranges must lie in the handle's own actors (a shard holds [lo, hi) only).
 int check_range(const Handle* h, int64_t first, int64_t count) {
-    if (first < 0 || count < 0 || first + count > (int64_t)h->g.actors)
-        return fail(GP_EINVAL, "range [%lld, %lld) outside 0..%u", (long long)first, (long long)(first + count), h->g.actors);
+    if (first < (int64_t)h->lo || count < 0 || first + count > (int64_t)h->hi)
+        return fail(GP_EINVAL, "range [%lld, %lld) outside this handle's actors [%u, %u)", (long long)first,
+                    (long long)(first + count), h->lo, h->hi);
     return GP_OK;
 }
 
@@ -466,18 +804,8 @@ int copy_slice(const Handle* h, std::vector<T>& out, const T* src, int64_t first
     return GP_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-int gp_abi_version(void) { return GP_ABI_VERSION; }
-
-int gp_sizes(int64_t n_arg, int32_t topology, int64_t* nodes, int64_t* actors, int64_t* grid) {
-    if (!nodes || !actors || !grid) return fail(GP_EINVAL, "null output pointer");
-    return sizes(n_arg, topology, nodes, actors, grid);
-}
-
-int gp_create(const gp_config* cfg, gp_layout* out, void** handle) {
+int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_layout* out, gp_shard_layout* shard,
+           void** handle) {
     if (!cfg || !handle) return fail(GP_EINVAL, "null argument");
     *handle = nullptr;
     if (cfg->algo != GP_GOSSIP && cfg->algo != GP_PUSHSUM) return fail(GP_EINVAL, "unknown algorithm %d", cfg->algo);
@@ -487,6 +815,16 @@ int gp_create(const gp_config* cfg, gp_layout* out, void** handle) {
     int64_t nodes, actors, grid;
     int rc = sizes(cfg->n_arg, cfg->topology, &nodes, &actors, &grid);
     if (rc) return rc;
+    std::vector<int64_t> bounds;
+    if (sharded) {
+        if (rank < 0 || rank >= world) return fail(GP_EINVAL, "rank %d outside 0..%d", rank, world - 1);
+        if (cfg->topology == GP_FULL && cfg->algo == GP_PUSHSUM)
+            return fail(GP_EINVAL, "push-sum on \"full\" runs on one GPU only (gp_create)");
+        if (cfg->flags & GP_FLAG_GENERIC) return fail(GP_EINVAL, "GP_FLAG_GENERIC is single-GPU only");
+        if ((rc = partition(cfg->n_arg, cfg->topology, world, bounds))) return rc;
+    } else {
+        bounds = {0, actors};
+    }
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (cfg->device < 0 || cfg->device >= ndev) return fail(GP_EINVAL, "device %d not present (%d devices)", cfg->device, ndev);
@@ -500,6 +838,12 @@ int gp_create(const gp_config* cfg, gp_layout* out, void** handle) {
     h->gossip = cfg->algo == GP_GOSSIP;
     h->full = cfg->topology == GP_FULL;
     h->generic = h->full || (cfg->flags & GP_FLAG_GENERIC);
+    h->sharded = sharded;
+    h->rank = sharded ? rank : 0;
+    h->world = sharded ? world : 1;
+    h->abnd = bounds;
+    h->lo = (uint32_t)bounds[h->rank];
+    h->hi = (uint32_t)bounds[h->rank + 1];
     Geom& g = h->g;
     g.actors = (uint32_t)actors;
     if (cfg->topology == GP_IMP3D || cfg->topology == GP_THREE_D) {
@@ -516,6 +860,7 @@ int gp_create(const gp_config* cfg, gp_layout* out, void** handle) {
     }
     g.dx = make_fastdiv(g.gx);
     g.dy = make_fastdiv(g.gy);
+    if (h->world > 1 && !h->full) h->halo = g.gz > 1 ? g.plane : 1u;  // grid rows crossing a shard face
     // leader = Random().Next(0, nodes)  (program.fs:173/211/250/316)
     h->lay.leader = scale_draw(philox(0u, 0u, kStreamLeader, cfg->seed).x, (uint32_t)nodes);
     int64_t part = 0;
@@ -524,18 +869,18 @@ int gp_create(const gp_config* cfg, gp_layout* out, void** handle) {
         for (int64_t v = 0; v < actors; ++v) part += presence(g, (uint32_t)v) != 0u;
     h->lay.participants = part;
     if (const char* ab = std::getenv("GP_ABLATE")) h->ablate = (uint32_t)std::strtoul(ab, nullptr, 0);
-    h->grid = grid_for(g.actors);
+    h->grid = grid_for(h->own());
     if (const char* gg = std::getenv("GP_GRID")) {  // tuning override (rounded to a multiple of 8)
         const long v = std::strtol(gg, nullptr, 0);
         if (v >= 8) h->grid = (int)((v + 7) / 8 * 8);
     }
-    h->span = span_for(g.actors, h->grid);
+    h->span = span_for(h->own(), h->grid);
 
     auto bail = [&](int code) {
         delete h;
         return code;
     };
-    if (cfg->stream) {
+    if (cfg->stream || (cfg->flags & GP_FLAG_USE_STREAM)) {
         h->stream = (hipStream_t)cfg->stream;
     } else {
         hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
@@ -545,19 +890,23 @@ int gp_create(const gp_config* cfg, gp_layout* out, void** handle) {
     if (hipEventCreate(&h->ev_a) != hipSuccess || hipEventCreate(&h->ev_b) != hipSuccess)
         return bail(fail(GP_EHIP, "hipEventCreate failed"));
 
-    const size_t A = (size_t)actors;
+    // own actors [lo, hi); round-to-round messages also for the halo rows of both neighbours
+    const size_t n = h->own(), A = (size_t)actors;
+    const int64_t lo = h->lo, xlo = h->ext_lo();
+    const size_t xn = (size_t)(h->ext_hi() - xlo);
     if (h->gossip) {
-        if ((rc = h->alloc(&h->cnt, A)) || (rc = h->alloc(&h->gstate, A))) return bail(rc);
+        if ((rc = h->alloc(&h->cnt, n, lo)) || (rc = h->alloc(&h->gstate, n, lo))) return bail(rc);
         if (h->generic) {
-            if ((rc = h->alloc(&h->inc[0], A)) || (rc = h->alloc(&h->inc[1], A))) return bail(rc);
-        } else if ((rc = h->alloc(&h->dir[0], A)) || (rc = h->alloc(&h->dir[1], A))) {
+            if ((rc = h->alloc(&h->inc[0], n, lo)) || (rc = h->alloc(&h->inc[1], n, lo))) return bail(rc);
+        } else if ((rc = h->alloc(&h->dir[0], xn, xlo)) || (rc = h->alloc(&h->dir[1], xn, xlo))) {
             return bail(rc);
         }
     } else {
-        if ((rc = h->alloc(&h->msg[0], A)) || (rc = h->alloc(&h->msg[1], A)) || (rc = h->alloc(&h->flags, A)) ||
-            (rc = h->alloc(&h->frozen, A)) || (rc = h->alloc(&h->partials, (size_t)h->grid)))
+        if ((rc = h->alloc(&h->msg[0], xn, xlo)) || (rc = h->alloc(&h->msg[1], xn, xlo)) ||
+            (rc = h->alloc(&h->flags, n, lo)) || (rc = h->alloc(&h->frozen, n, lo)) ||
+            (rc = h->alloc(&h->partials, (size_t)h->grid)))
             return bail(rc);
-        if (h->generic) {
+        if (h->generic) {  // single-GPU only: whole graph
             for (int i = 0; i < 2; ++i)
                 if ((rc = h->alloc(&h->bcnt[i], A)) || (rc = h->alloc(&h->boff[i], A + 1)) ||
                     (rc = h->alloc(&h->slot[i], A)))
@@ -565,18 +914,85 @@ int gp_create(const gp_config* cfg, gp_layout* out, void** handle) {
             if ((rc = h->alloc(&h->tgt, A)) || (rc = h->alloc(&h->pos, A)) ||
                 (rc = h->alloc(&h->scan_scratch, scan_scratch_words((uint32_t)A))))
                 return bail(rc);
-        } else if ((rc = h->alloc(&h->dir[0], A)) || (rc = h->alloc(&h->dir[1], A))) {
+        } else if ((rc = h->alloc(&h->dir[0], xn, xlo)) || (rc = h->alloc(&h->dir[1], xn, xlo))) {
             return bail(rc);
         }
     }
     if (g.has_link && (rc = build_links(h))) return bail(rc);
+    if (h->sharded && (rc = build_plan(h))) return bail(rc);
     if ((rc = h->alloc(&h->parts, (size_t)kPartRing * kParts * kPartStride))) return bail(rc);
     if ((rc = ensure_trace(h, 4096))) return bail(rc);
     if ((rc = reset(h))) return bail(rc);
     h->lay.device_bytes = (int64_t)h->dev_bytes;
     if (out) *out = h->lay;
+    if (shard) {
+        shard->lo = h->lo;
+        shard->hi = h->hi;
+        shard->halo = h->halo;
+        shard->send_total = h->send_total;
+        shard->recv_total = h->recv_total;
+    }
     *handle = h;
     return GP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gp_abi_version(void) { return GP_ABI_VERSION; }
+
+int gp_sizes(int64_t n_arg, int32_t topology, int64_t* nodes, int64_t* actors, int64_t* grid) {
+    if (!nodes || !actors || !grid) return fail(GP_EINVAL, "null output pointer");
+    return sizes(n_arg, topology, nodes, actors, grid);
+}
+
+
+int gp_create(const gp_config* cfg, gp_layout* out, void** handle) {
+    return create(cfg, 0, 1, false, out, nullptr, handle);
+}
+
+int gp_create_shard(const gp_config* cfg, int32_t rank, int32_t world, gp_layout* out, gp_shard_layout* shard,
+                    void** handle) {
+    return create(cfg, rank, world, true, out, shard, handle);
+}
+
+int gp_partition(int64_t n_arg, int32_t topology, int32_t world, int64_t* bounds) {
+    if (!bounds) return fail(GP_EINVAL, "null bounds");
+    std::vector<int64_t> b;
+    const int rc = partition(n_arg, topology, world, b);
+    if (rc) return rc;
+    std::copy(b.begin(), b.end(), bounds);
+    return GP_OK;
+}
+
+int gp_shard_plan(void* handle, int64_t* send_bytes, int64_t* recv_bytes) {
+    if (!handle || !send_bytes || !recv_bytes) return fail(GP_EINVAL, "null argument");
+    Handle* h = H(handle);
+    if (!h->sharded) return fail(GP_ESTATE, "not a shard handle");
+    for (int q = 0; q < h->world; ++q) {
+        send_bytes[q] = (int64_t)h->out_chunk[q].size;
+        recv_bytes[q] = (int64_t)h->in_chunk[q].size;
+    }
+    return GP_OK;
+}
+
+int gp_shard_round(void* handle, void* send_buf) {
+    if (!handle) return fail(GP_EINVAL, "null handle");
+    if (!H(handle)->sharded) return fail(GP_ESTATE, "not a shard handle");
+    return shard_round(H(handle), send_buf);
+}
+
+int gp_shard_deliver(void* handle, const void* recv_buf) {
+    if (!handle) return fail(GP_EINVAL, "null handle");
+    if (!H(handle)->sharded) return fail(GP_ESTATE, "not a shard handle");
+    return shard_deliver(H(handle), recv_buf);
+}
+
+int gp_shard_sync(void* handle, gp_status* st) {
+    if (!handle) return fail(GP_EINVAL, "null handle");
+    if (!H(handle)->sharded) return fail(GP_ESTATE, "not a shard handle");
+    return shard_sync(H(handle), st);
 }
 
 int gp_reset(void* handle) {
@@ -704,9 +1120,12 @@ int gp_kernel_stats(void* handle, gp_kstats* out, int32_t reset_counters) {
     out->avg_ms = h->k_launches ? h->k_total_ms / (double)h->k_launches : 0.0;
     out->bytes_per_launch = bytes_per_round(h);
     std::snprintf(out->kernel, sizeof out->kernel, "%s", round_kernel_name(h));
+    out->aux_avg_ms = h->k_launches ? h->k_aux_ms / (double)h->k_launches : 0.0;
+    std::snprintf(out->aux_kernel, sizeof out->aux_kernel, "%s", aux_kernel_name(h));
     if (reset_counters) {
         h->k_launches = 0;
         h->k_total_ms = 0.0;
+        h->k_aux_ms = 0.0;
     }
     return GP_OK;
 }

@@ -11,6 +11,7 @@ constexpr int kPartStride = 16;     // u32 words between sub-counters
 constexpr int kPartRing = 4;        // rounds kept in the sub-counter ring
 // empty link slot: w holds this quiet-NaN bit pattern (a real weight is finite and >= 0)
 constexpr unsigned long long kEmptySlot = 0x7FF800000000DEADull;
+constexpr int kMaxWorld = 16;       // ranks of a sharded run (one per GPU; 8 on an MI355X node)
 
 // One synchronous round kernel F(r) fuses phase 2 of round r-1 (collect the messages sent to
 // this actor, read from the round r-1 buffers) with phase 1 of round r (update, convergence
@@ -18,6 +19,10 @@ constexpr unsigned long long kEmptySlot = 0x7FF800000000DEADull;
 struct RoundArgs {
     Geom g;
     uint64_t seed;
+    uint32_t lo, hi;       // actors this kernel updates: [0, actors), or a shard's node range
+    uint32_t slot_lo;      // first link slot held here (0, or the shard's first): the in-bounds
+                           // fallback index of predicated-off link-slot loads
+    uint32_t sharded;      // completion counts come from the exchange (total[] is global)
     uint32_t r;            // round index
     uint32_t target;       // completion target T = nodes (program.fs:178, AllNodes)
     uint32_t full;         // full topology (implicit k + (k >= v) neighbour map)
@@ -62,6 +67,42 @@ struct RoundArgs {
     uint32_t* pos_cur;        // slot of v's message inside its destination bucket
 };
 
+// Shard exchange (gp_shard_*).  Send chunk to peer q (built by this rank) and receive chunk from
+// peer q (built by q for this rank) share one layout: a 256-byte header, the halo face (direction
+// bytes, then push-sum messages) when q is a z-neighbour, then `cap` link entries: u32 slot (global
+// link-CSR slot; gossip: slot | (chains-1) << 31; full gossip: the target actor), then push-sum
+// (s, w) pairs.  See DESIGN.md §6.
+struct ShardHeader {
+    unsigned long long newly;  // actors that reported in the round (sender's range)
+    uint32_t nlinks;           // link entries written (<= cap)
+    uint32_t overflow;         // sender dropped entries: the run is void (GP_EOVERFLOW)
+};
+
+struct PeerOut {
+    ShardHeader* hdr;
+    uint32_t* slot;
+    double2* msg;
+    uint32_t cap;
+};
+
+struct PeerIn {
+    const ShardHeader* hdr;
+    const uint32_t* slot;
+    const double2* msg;
+    uint32_t cap;
+};
+
+struct Xchg {
+    uint32_t world, rank;
+    uint32_t abnd[kMaxWorld + 1];  // actor range of every rank
+    uint32_t sbnd[kMaxWorld + 1];  // link-slot range of every rank (global CSR numbering)
+    uint32_t* pcount;              // per-peer entry counters of the current round (zeroed by pack)
+    uint32_t* overflow;            // sticky local overflow flag
+    unsigned long long* self_newly;  // this rank's count of the round (pack -> unpack)
+    PeerOut out[kMaxWorld];
+    PeerIn in[kMaxWorld];
+};
+
 struct Launch {
     int grid;
     hipStream_t stream;
@@ -78,6 +119,18 @@ void launch_gs_link_scatter(const RoundArgs& a, const Launch& l);
 void launch_ps_push_emit(const RoundArgs& a, const Launch& l);
 void launch_ps_push_fill(const RoundArgs& a, uint32_t* slot_cur, const uint32_t* boff_cur, const Launch& l);
 void launch_gs_push(const RoundArgs& a, const Launch& l);
+// sharded variants: remote link / full-topology messages go to the send chunks of x
+void launch_ps_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);
+void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);
+void launch_gs_push_x(const RoundArgs& a, const Xchg& x, const Launch& l);
+// headers of round `applied` (-1: none) into every send chunk; zero the per-peer counters
+void launch_shard_pack(const RoundArgs& a, const Xchg& x, long long applied, hipStream_t s);
+// total[applied] from the headers; link entries into lmsg_cur / lcnt_cur / inc_cur
+void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, uint32_t max_cap, int gossip,
+                         int full, hipStream_t s);
+// per-(source rank, destination rank, degree) counts of extra links, for the exchange plan
+void launch_link_hist(const uint32_t* link, const Geom& g, const Xchg& x, unsigned long long* hist,
+                      const Launch& l);
 
 // setup / utility kernels
 void launch_links(uint32_t* link, uint32_t nodes, uint64_t seed, const Launch& l);
@@ -93,7 +146,8 @@ void launch_fill_u8(uint8_t* p, uint8_t v, size_t n, hipStream_t s);
 void launch_fill_empty_slots(double2* p, size_t n, hipStream_t s);
 // total[a] = total[a-1] + sum of the round-a sub-counters (after the last kernel of a batch)
 void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hipStream_t s);
-void launch_ps_init(uint8_t* flags, const Geom& g, uint32_t full, uint32_t term_init, const Launch& l);
+void launch_ps_init(uint8_t* flags, const Geom& g, uint32_t lo, uint32_t hi, uint32_t full, uint32_t term_init,
+                    const Launch& l);
 // push-sum sums for gp_status: per-block partials of held + in-flight (s, w)
 void launch_ps_sums(const RoundArgs& a, uint32_t last_round_valid, double2* partials, const Launch& l);
 

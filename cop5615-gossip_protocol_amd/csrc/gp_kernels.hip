@@ -20,14 +20,14 @@ namespace gp {
 
 namespace {
 
-__device__ __forceinline__ void node_range(uint32_t n, uint32_t span, uint32_t& v, uint32_t& end,
+__device__ __forceinline__ void node_range(uint32_t lo, uint32_t hi, uint32_t span, uint32_t& v, uint32_t& end,
                                            uint32_t& step) {
     const uint32_t grp = blockIdx.x & 7u;
     const uint32_t j = blockIdx.x >> 3;
     const uint32_t per = gridDim.x >> 3;
-    const uint32_t base = grp * span;
-    end = base + span < n ? base + span : n;
-    if (base >= n) end = 0;
+    const uint32_t base = lo + grp * span;
+    end = base + span < hi ? base + span : hi;
+    if (base >= hi) end = 0;
     v = base + j * kBlock + threadIdx.x;
     step = per * kBlock;
 }
@@ -55,18 +55,23 @@ __device__ __forceinline__ void block_add(uint32_t c, uint32_t* parts, long long
 // Skip gate of a kernel that applies round `a`: the completion count after round a-1 is
 // total[a-2] + the round a-1 sub-counters, all final (earlier launches).  Every block computes
 // it (one wave, 64 loads), so every block takes the same branch; block 0 publishes total[a-1]
-// and empties the ring slot that round a+2 will use.
+// and empties the ring slot that round a+2 will use.  Sharded: total[a-1] is the global count,
+// already written by the exchange's unpack (k_shard_unpack).
 __device__ __forceinline__ bool gate(const RoundArgs& A, long long a) {
     __shared__ unsigned long long prev_s;
     if (threadIdx.x < 64) {
-        unsigned long long x = 0;
-        if (a >= 1) x = *part_slot(A.parts, a - 1, threadIdx.x);
+        if (A.sharded) {
+            if (threadIdx.x == 0) prev_s = a >= 1 ? A.total[a - 1] : 0ull;
+        } else {
+            unsigned long long x = 0;
+            if (a >= 1) x = *part_slot(A.parts, a - 1, threadIdx.x);
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-        if (threadIdx.x == 0) {
-            if (a >= 2) x += A.total[a - 2];
-            prev_s = x;
-            if (blockIdx.x == 0 && a >= 1) A.total[a - 1] = x;
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+            if (threadIdx.x == 0) {
+                if (a >= 2) x += A.total[a - 2];
+                prev_s = x;
+                if (blockIdx.x == 0 && a >= 1) A.total[a - 1] = x;
+            }
         }
         if (blockIdx.x == 0) *part_slot(A.parts, a + 2, threadIdx.x) = 0u;
     }
@@ -153,7 +158,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
     const Geom g = a.g;
     const uint32_t r = a.r;
     uint32_t v, end, step;
-    node_range(g.actors, a.span, v, end, step);
+    node_range(a.lo, a.hi, a.span, v, end, step);
     uint32_t newly = 0;
     for (; v < end; v += step) {
         const uint32_t m = presence(g, v);
@@ -219,8 +224,8 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
                 uint32_t ls[kLinkUnroll];
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) {
-                    lm[k] = load_sel(a.lmsg_prev, k < nl, li + k, 0u);
-                    ls[k] = load_sel(a.rev_src, k < nl, li + k, 0u);
+                    lm[k] = load_sel(a.lmsg_prev, k < nl, li + k, a.slot_lo);
+                    ls[k] = load_sel(a.rev_src, k < nl, li + k, a.slot_lo);
                 }
                 // merge: link slots are sorted by source; a sender matches grid OR link, never both
 #pragma unroll
@@ -266,7 +271,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
     const Geom g = a.g;
     const uint32_t r = a.r;
     uint32_t v, end, step;
-    node_range(g.actors, a.span, v, end, step);
+    node_range(a.lo, a.hi, a.span, v, end, step);
     uint32_t newly = 0;
     for (; v < end; v += step) {
         const uint32_t m = presence(g, v);
@@ -285,7 +290,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
                 const uint32_t li = a.rev_off[v], nl = a.rev_off[v + 1] - li;
                 uint8_t lc[kLinkUnroll];
 #pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, 0u);
+                for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, a.slot_lo);
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k)
                     if (k < nl && lc[k]) {
@@ -370,6 +375,174 @@ __global__ __launch_bounds__(kBlock) void k_gs_link_scatter(RoundArgs a) {
         if (nl[j]) a.lcnt_cur[lp[j]] = (uint8_t)nl[j];
 }
 
+// ------------------------------------------------------------------ shard exchange
+// Owner rank of x under the range bounds b[0..world] (world <= 16: a short uniform loop).
+__device__ __forceinline__ uint32_t owner(const uint32_t* b, uint32_t world, uint32_t x) {
+    uint32_t q = 0;
+    for (uint32_t i = 1; i < world; ++i) q += x >= b[i] ? 1u : 0u;
+    return q;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// Position of this lane's entry in peer q's send chunk: one atomic per distinct peer per wave
+// (ballot + mbcnt), not one per entry.  Every active lane of the wave must call it.
+__device__ __forceinline__ uint32_t reserve(const Xchg& x, bool want, uint32_t q) {
+    unsigned long long pending = __ballot(want);
+    uint32_t pos = 0;
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const uint32_t qq = __shfl(q, leader, 64);
+        const bool mine = want && q == qq;
+        const unsigned long long mask = __ballot(mine);
+        uint32_t base = 0;
+        if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(&x.pcount[qq], (uint32_t)__popcll(mask));
+        base = __shfl(base, leader, 64);
+        if (mine) pos = base + lanes_below(mask);
+        pending &= ~mask;
+    }
+    return pos;
+}
+
+// Append (entry, msg) to peer q's chunk at pos, or flag the overflow (never silently dropped:
+// gp_shard_sync fails the run with GP_EOVERFLOW).
+template <bool MSG>
+__device__ __forceinline__ void put(const Xchg& x, uint32_t q, uint32_t pos, uint32_t entry, double2 m) {
+    const PeerOut& o = x.out[q];
+    if (pos < o.cap) {
+        o.slot[pos] = entry;
+        if (MSG) o.msg[pos] = m;
+    } else {
+        atomicOr(x.overflow, 1u);
+    }
+}
+
+// Sharded k_ps_link_scatter: link messages whose CSR slot belongs to another rank go to that
+// rank's send chunk as (global slot, s, w); the receiver writes them into the same slot.
+__global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg x) {
+    const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
+    const uint32_t base = a.lo + blockIdx.x * kBlock * kScatterPer + threadIdx.x;
+    const uint32_t slo = x.sbnd[x.rank], shi = x.sbnd[x.rank + 1];
+    bool l[kScatterPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j) {
+        const uint32_t u = base + j * kBlock;
+        l[j] = u < n && load_sel(a.dir_cur, u < n, u, a.lo) == kDirLink;
+    }
+    uint32_t lp[kScatterPer];
+    double2 mm[kScatterPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j) {
+        const uint32_t u = base + j * kBlock;
+        lp[j] = load_sel(a.lpos, l[j], u, a.lo);
+        mm[j] = load_sel(a.msg_cur, l[j], u, a.lo);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j) {
+        const bool remote = l[j] && (lp[j] < slo || lp[j] >= shi);
+        if (l[j] && !remote) a.lmsg_cur[lp[j]] = mm[j];
+        const uint32_t q = remote ? owner(x.sbnd, x.world, lp[j]) : 0u;
+        const uint32_t pos = reserve(x, remote, q);
+        if (remote) put<true>(x, q, pos, lp[j], mm[j]);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_gs_link_scatter_x(RoundArgs a, Xchg x) {
+    const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
+    const uint32_t base = a.lo + blockIdx.x * kBlock * kScatterPer + threadIdx.x;
+    const uint32_t slo = x.sbnd[x.rank], shi = x.sbnd[x.rank + 1];
+    uint32_t nl[kScatterPer], lp[kScatterPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j) {
+        const uint32_t u = base + j * kBlock;
+        const uint8_t b = load_sel(a.dir_cur, u < n, u, a.lo);
+        nl[j] = u < n ? (uint32_t)((b & 15u) == kDirLink) + (uint32_t)((b >> 4) == kDirLink) : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j) lp[j] = load_sel(a.lpos, nl[j] != 0u, base + j * kBlock, a.lo);
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j) {
+        const bool remote = nl[j] && (lp[j] < slo || lp[j] >= shi);
+        if (nl[j] && !remote) a.lcnt_cur[lp[j]] = (uint8_t)nl[j];
+        const uint32_t q = remote ? owner(x.sbnd, x.world, lp[j]) : 0u;
+        const uint32_t pos = reserve(x, remote, q);
+        if (remote) put<false>(x, q, pos, lp[j] | ((nl[j] - 1u) << 31), make_double2(0.0, 0.0));
+    }
+}
+
+// Round `applied`'s count into every send header; the per-peer counters restart at 0.
+__global__ void k_shard_pack(RoundArgs a, Xchg x, long long applied) {
+    unsigned long long newly = 0;
+    if (applied >= 0) newly = *part_slot(a.parts, applied, threadIdx.x);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) newly += __shfl_xor(newly, off, 64);
+    if (threadIdx.x == 0) *x.self_newly = newly;
+    const uint32_t q = threadIdx.x;
+    if (q < x.world && q != x.rank) {
+        const uint32_t c = x.pcount[q];
+        ShardHeader h;
+        h.newly = newly;
+        h.nlinks = c < x.out[q].cap ? c : x.out[q].cap;
+        h.overflow = (c > x.out[q].cap || *x.overflow) ? 1u : 0u;
+        *x.out[q].hdr = h;
+        x.pcount[q] = 0u;
+    }
+}
+
+// total[applied] = total[applied-1] + every rank's count; the received link entries land in
+// their CSR slots (push-sum (s,w) / gossip chain count) or, for "full" gossip, as receipts.
+__global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, long long applied, int gossip,
+                                                          int full) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && applied >= 0) {
+        unsigned long long t = *x.self_newly;
+        uint32_t of = 0;
+        for (uint32_t q = 0; q < x.world; ++q)
+            if (q != x.rank) {
+                t += x.in[q].hdr->newly;
+                of |= x.in[q].hdr->overflow;
+            }
+        a.total[applied] = (applied >= 1 ? a.total[applied - 1] : 0ull) + t;
+        if (of) atomicOr(x.overflow, 1u);
+    }
+    // an entry outside this rank's actors / slots can only come from a corrupt chunk: it is
+    // reported (GP_EOVERFLOW at the next sync), never written
+    const uint32_t elo = full ? a.lo : x.sbnd[x.rank], ehi = full ? a.hi : x.sbnd[x.rank + 1];
+    for (uint32_t q = 0; q < x.world; ++q) {
+        if (q == x.rank) continue;
+        const PeerIn& in = x.in[q];
+        uint32_t n = in.hdr->nlinks;
+        n = n < in.cap ? n : in.cap;
+        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+            const uint32_t e = in.slot[i];
+            const uint32_t t = (gossip && !full) ? e & 0x7FFFFFFFu : e;
+            if (t < elo || t >= ehi) {
+                atomicOr(x.overflow, 2u);
+                continue;
+            }
+            if (full) atomicAdd(&a.inc_cur[t], 1u);
+            else if (gossip) a.lcnt_cur[t] = (uint8_t)((e >> 31) + 1u);
+            else a.lmsg_cur[t] = in.msg[i];
+        }
+    }
+}
+
+// hist[(src rank * world + dst rank) * 8 + degree] over every extra link (LDS-privatised).
+__global__ __launch_bounds__(kBlock) void k_link_hist(const uint32_t* link, Geom g, Xchg x, unsigned long long* hist) {
+    __shared__ uint32_t h[kMaxWorld * kMaxWorld * 8];
+    const uint32_t nb = x.world * x.world * 8;
+    for (uint32_t i = threadIdx.x; i < nb; i += kBlock) h[i] = 0;
+    __syncthreads();
+    for (uint32_t u = blockIdx.x * kBlock + threadIdx.x; u < g.wired; u += gridDim.x * kBlock) {
+        const uint32_t sp = owner(x.abnd, x.world, u), dp = owner(x.abnd, x.world, link[u]);
+        atomicAdd(&h[(sp * x.world + dp) * 8 + popc(presence(g, u))], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nb; i += kBlock)
+        if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
+}
+
 // ------------------------------------------------------------------ generic (bucketed) paths
 __device__ __forceinline__ uint32_t generic_deg(const RoundArgs& a, uint32_t v, uint32_t& m) {
     if (a.full) {
@@ -388,11 +561,12 @@ __device__ __forceinline__ uint32_t generic_target(const RoundArgs& a, uint32_t 
 
 // Gossip on any topology (used for "full"): receipts are integer atomics into inc_cur[t]
 // (order-free, so exact); the done filter of program.fs:92 is applied receiver-side.
-__global__ __launch_bounds__(kBlock) void k_gs_push(RoundArgs a) {
+template <bool X>
+__device__ __forceinline__ void gs_push_body(const RoundArgs& a, const Xchg* xp) {
     if (a.r && gate(a, (long long)a.r - 1)) return;
     const uint32_t r = a.r;
     uint32_t v, end, step;
-    node_range(a.g.actors, a.span, v, end, step);
+    node_range(a.lo, a.hi, a.span, v, end, step);
     uint32_t newly = 0;
     for (; v < end; v += step) {
         uint32_t m;
@@ -417,14 +591,37 @@ __global__ __launch_bounds__(kBlock) void k_gs_push(RoundArgs a) {
                 }
             }
         }
-        if (tok) {
-            const uint4 x = philox(v, r, kStreamGossip, a.seed);
-            atomicAdd(&a.inc_cur[generic_target(a, v, m, scale_draw(x.x, d))], 1u);
-            if (tok > 1) atomicAdd(&a.inc_cur[generic_target(a, v, m, scale_draw(x.y, d))], 1u);
+        if (!X) {
+            if (tok) {
+                const uint4 px = philox(v, r, kStreamGossip, a.seed);
+                atomicAdd(&a.inc_cur[generic_target(a, v, m, scale_draw(px.x, d))], 1u);
+                if (tok > 1) atomicAdd(&a.inc_cur[generic_target(a, v, m, scale_draw(px.y, d))], 1u);
+            }
+        } else {  // receipts for another rank's actors go to its send chunk (the target id)
+            const Xchg& x = *xp;
+            uint32_t t[2] = {0u, 0u};
+            if (tok) {
+                const uint4 px = philox(v, r, kStreamGossip, a.seed);
+                t[0] = generic_target(a, v, m, scale_draw(px.x, d));
+                t[1] = generic_target(a, v, m, scale_draw(px.y, d));
+            }
+#pragma unroll
+            for (uint32_t c = 0; c < 2; ++c) {
+                const bool send = tok > c;
+                const bool remote = send && (t[c] < a.lo || t[c] >= a.hi);
+                if (send && !remote) atomicAdd(&a.inc_cur[t[c]], 1u);
+                const uint32_t q = remote ? owner(x.abnd, x.world, t[c]) : 0u;
+                const uint32_t pos = reserve(x, remote, q);
+                if (remote) put<false>(x, q, pos, t[c], make_double2(0.0, 0.0));
+            }
         }
     }
     if (r) block_add(newly, a.parts, (long long)r - 1);
 }
+
+__global__ __launch_bounds__(kBlock) void k_gs_push(RoundArgs a) { gs_push_body<false>(a, nullptr); }
+
+__global__ __launch_bounds__(kBlock) void k_gs_push_x(RoundArgs a, Xchg x) { gs_push_body<true>(a, &x); }
 
 // Push-sum on any topology (used for "full"): messages are bucketed by destination with an
 // integer atomic (slot order is arbitrary), then each receiver visits its bucket in ascending
@@ -434,7 +631,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_push_emit(RoundArgs a) {
     if (gate(a, a.r)) return;
     const uint32_t r = a.r;
     uint32_t v, end, step;
-    node_range(a.g.actors, a.span, v, end, step);
+    node_range(a.lo, a.hi, a.span, v, end, step);
     uint32_t newly = 0;
     for (; v < end; v += step) {
         uint32_t m;
@@ -489,7 +686,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_push_fill(RoundArgs a, uint32_t* 
     if (a.r) prev = a.total[a.r - 1];
     if (prev >= a.target) return;
     uint32_t v, end, step;
-    node_range(a.g.actors, a.span, v, end, step);
+    node_range(a.lo, a.hi, a.span, v, end, step);
     for (; v < end; v += step) {
         const uint32_t t = a.tgt_cur[v];
         if (t != 0xFFFFFFFFu) slot_cur[boff_cur[t] + a.pos_cur[v]] = v;
@@ -624,8 +821,8 @@ __global__ void k_finalize(unsigned long long* total, uint32_t* parts, long long
     if (threadIdx.x == 0) total[a] = x + (a >= 1 ? total[a - 1] : 0ull);
 }
 
-__global__ void k_ps_init(uint8_t* flags, Geom g, uint32_t full, uint32_t term_init) {
-    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < g.actors; v += gridDim.x * blockDim.x) {
+__global__ void k_ps_init(uint8_t* flags, Geom g, uint32_t lo, uint32_t hi, uint32_t full, uint32_t term_init) {
+    for (uint32_t v = lo + blockIdx.x * blockDim.x + threadIdx.x; v < hi; v += gridDim.x * blockDim.x) {
         const bool part = full ? true : presence(g, v) != 0u;
         flags[v] = part ? (uint8_t)term_init : (uint8_t)0;  // termRound = 1 (program.fs:79)
     }
@@ -635,7 +832,7 @@ __global__ void k_ps_init(uint8_t* flags, Geom g, uint32_t full, uint32_t term_i
 __global__ __launch_bounds__(kBlock) void k_ps_sums(RoundArgs a, uint32_t valid, double2* partials) {
     __shared__ double2 red[kBlock];
     double s = 0.0, w = 0.0;
-    for (uint32_t v = blockIdx.x * kBlock + threadIdx.x; v < a.g.actors; v += gridDim.x * kBlock) {
+    for (uint32_t v = a.lo + blockIdx.x * kBlock + threadIdx.x; v < a.hi; v += gridDim.x * kBlock) {
         uint32_t m;
         if (!generic_deg(a, v, m)) continue;
         const uint8_t f = a.flags[v];
@@ -713,6 +910,39 @@ void launch_gs_push(const RoundArgs& a, const Launch& l) {
     hipLaunchKernelGGL(k_gs_push, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
 }
 
+static unsigned scatter_blocks(const RoundArgs& a) {
+    const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
+    return n > a.lo ? (n - a.lo + kScatterPer * kBlock - 1) / (kScatterPer * kBlock) : 0u;
+}
+
+void launch_ps_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l) {
+    if (const unsigned b = scatter_blocks(a)) hipLaunchKernelGGL(k_ps_link_scatter_x, dim3(b), dim3(kBlock), 0, l.stream, a, x);
+}
+
+void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l) {
+    if (const unsigned b = scatter_blocks(a)) hipLaunchKernelGGL(k_gs_link_scatter_x, dim3(b), dim3(kBlock), 0, l.stream, a, x);
+}
+
+void launch_gs_push_x(const RoundArgs& a, const Xchg& x, const Launch& l) {
+    hipLaunchKernelGGL(k_gs_push_x, dim3(l.grid), dim3(kBlock), 0, l.stream, a, x);
+}
+
+void launch_shard_pack(const RoundArgs& a, const Xchg& x, long long applied, hipStream_t s) {
+    hipLaunchKernelGGL(k_shard_pack, dim3(1), dim3(64), 0, s, a, x, applied);
+}
+
+void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, uint32_t max_cap, int gossip,
+                         int full, hipStream_t s) {
+    uint32_t blocks = (max_cap + kBlock - 1) / kBlock;
+    blocks = blocks < 1u ? 1u : (blocks > (uint32_t)kMaxGrid ? (uint32_t)kMaxGrid : blocks);
+    hipLaunchKernelGGL(k_shard_unpack, dim3(blocks), dim3(kBlock), 0, s, a, x, applied, gossip, full);
+}
+
+void launch_link_hist(const uint32_t* link, const Geom& g, const Xchg& x, unsigned long long* hist,
+                      const Launch& l) {
+    hipLaunchKernelGGL(k_link_hist, dim3(l.grid), dim3(kBlock), 0, l.stream, link, g, x, hist);
+}
+
 void launch_links(uint32_t* link, uint32_t nodes, uint64_t seed, const Launch& l) {
     hipLaunchKernelGGL(k_links, dim3(l.grid), dim3(kBlock), 0, l.stream, link, nodes, seed);
 }
@@ -762,8 +992,9 @@ void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hi
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, total, parts, a);
 }
 
-void launch_ps_init(uint8_t* flags, const Geom& g, uint32_t full, uint32_t term_init, const Launch& l) {
-    hipLaunchKernelGGL(k_ps_init, dim3(l.grid), dim3(kBlock), 0, l.stream, flags, g, full, term_init);
+void launch_ps_init(uint8_t* flags, const Geom& g, uint32_t lo, uint32_t hi, uint32_t full, uint32_t term_init,
+                    const Launch& l) {
+    hipLaunchKernelGGL(k_ps_init, dim3(l.grid), dim3(kBlock), 0, l.stream, flags, g, lo, hi, full, term_init);
 }
 
 void launch_ps_sums(const RoundArgs& a, uint32_t valid, double2* partials, const Launch& l) {

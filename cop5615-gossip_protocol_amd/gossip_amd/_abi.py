@@ -12,12 +12,13 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, "lib", "libgossip_hip.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "gossip_hip.h")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 TOPOLOGIES = {"line": 0, "full": 1, "2D": 2, "Imp3D": 3, "3D": 4}
 ALGOS = {"gossip": 0, "push-sum": 1}
 FLAG_KERNEL_TIMING = 1
 FLAG_GENERIC = 2
-ERRORS = {-1: "GP_EINVAL", -2: "GP_ENOMEM", -3: "GP_EHIP", -4: "GP_ESTATE"}
+FLAG_USE_STREAM = 4
+ERRORS = {-1: "GP_EINVAL", -2: "GP_ENOMEM", -3: "GP_EHIP", -4: "GP_ESTATE", -5: "GP_EOVERFLOW"}
 
 
 class Config(C.Structure):
@@ -41,12 +42,19 @@ class Status(C.Structure):
 
 class KStats(C.Structure):
     _fields_ = [("launches", C.c_int64), ("total_ms", C.c_double), ("avg_ms", C.c_double),
-                ("bytes_per_launch", C.c_double), ("kernel", C.c_char * 64)]
+                ("bytes_per_launch", C.c_double), ("kernel", C.c_char * 64),
+                ("aux_avg_ms", C.c_double), ("aux_kernel", C.c_char * 64)]
+
+
+class ShardLayout(C.Structure):
+    _fields_ = [("lo", C.c_int64), ("hi", C.c_int64), ("halo", C.c_int64),
+                ("send_total", C.c_int64), ("recv_total", C.c_int64)]
 
 
 EXPORTS = ["gp_abi_version", "gp_sizes", "gp_create", "gp_reset", "gp_step", "gp_read_gossip",
            "gp_read_pushsum", "gp_read_messages", "gp_read_trace", "gp_neighbors",
-           "gp_kernel_stats", "gp_destroy", "gp_last_error"]
+           "gp_kernel_stats", "gp_partition", "gp_create_shard", "gp_shard_plan", "gp_shard_round",
+           "gp_shard_deliver", "gp_shard_sync", "gp_destroy", "gp_last_error"]
 
 
 class GossipError(RuntimeError):
@@ -63,6 +71,12 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise GossipError(f"HIP engine not built: {LIB_PATH} missing (run __graft_entry__.build())")
+    # One HIP runtime per process: torch bundles its own libamdhip64 / libhsa-runtime64 with the
+    # same sonames as /opt/rocm's.  Loaded first, they satisfy this library's dependencies, so
+    # kernels, streams and RCCL buffers all live in torch's runtime.  Loading ours first would
+    # bring a second runtime into the process, and one of the two then finds no device.
+    import torch  # noqa: F401
+
     L = C.CDLL(LIB_PATH)
     P = C.c_void_p
     L.gp_abi_version.restype = C.c_int
@@ -76,6 +90,13 @@ def load():
     L.gp_read_trace.argtypes = [P, C.c_int64, C.c_int64, P]
     L.gp_neighbors.argtypes = [P, C.c_int64, P, C.c_int32]
     L.gp_kernel_stats.argtypes = [P, C.POINTER(KStats), C.c_int32]
+    L.gp_partition.argtypes = [C.c_int64, C.c_int32, C.c_int32, P]
+    L.gp_create_shard.argtypes = [C.POINTER(Config), C.c_int32, C.c_int32, C.POINTER(Layout),
+                                  C.POINTER(ShardLayout), C.POINTER(C.c_void_p)]
+    L.gp_shard_plan.argtypes = [P, P, P]
+    L.gp_shard_round.argtypes = [P, P]
+    L.gp_shard_deliver.argtypes = [P, P]
+    L.gp_shard_sync.argtypes = [P, C.POINTER(Status)]
     L.gp_destroy.argtypes = [P]
     L.gp_destroy.restype = None
     L.gp_last_error.restype = C.c_char_p

@@ -1,0 +1,222 @@
+"""Multi-GPU host: one graph split into node-range shards, one process (or handle) per GPU.
+
+The reference has no distributed mode: its only parallelism is the Akka dispatcher running
+the actors on the .NET thread pool (program.fs:23), and the ParentActor counts reports until
+`AllNodes` (program.fs:44-63).  Here every rank owns a contiguous actor range
+(``gp_partition``: whole z-planes for Imp3D/3D) and one round is
+
+    engine.round()          # F(k) on this rank's actors + pack what other ranks need
+    transport.exchange()    # ONE all-to-all with sizes fixed at creation (RCCL over xGMI)
+    engine.deliver()        # unpack: halo faces, cross-shard link messages, global count
+
+with everything enqueued on the engine's HIP stream — the host only waits every few rounds
+(``engine.sync()``) to learn whether the global completion count reached `nodes`.
+
+Engines: :class:`HipShard` (libgossip_hip.so on a GPU — the product) and, in the tests,
+``oracle.OracleShard`` (the CPU checker).  Transports: :class:`TorchTransport`
+(torch.distributed all_to_all_single: RCCL for CUDA tensors, gloo for CPU tensors) and
+:class:`LoopbackTransport` (several shards inside one process).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+
+
+def partition(n_arg: int, topology: str, world: int):
+    """Actor bounds of every rank (gp_partition): list of world+1 ints."""
+    b = np.zeros(world + 1, np.int64)
+    _abi.check(_abi.load().gp_partition(n_arg, _abi.TOPOLOGIES[topology], world,
+                                        b.ctypes.data_as(C.c_void_p)))
+    return [int(x) for x in b]
+
+
+class HipShard:
+    """Rank `rank` of `world` on HIP device `device` (gp_create_shard)."""
+
+    def __init__(self, n_arg: int, topology: str, algorithm: str, *, rank: int, world: int, seed: int = 1,
+                 device: int = 0, stream: int | None = None, kernel_timing: bool = False, delta: float = 1e-10,
+                 gossip_threshold: int = 10, term_init: int = 1, term_limit: int = 3):
+        import torch
+
+        if topology not in _abi.TOPOLOGIES:
+            raise ValueError(f"unknown topology {topology!r} (case-sensitive: {list(_abi.TOPOLOGIES)})")
+        if algorithm not in _abi.ALGOS:
+            raise ValueError("Invalid:Please enter a proper protocol or topology")
+        self.lib = _abi.load()
+        # torch's current stream by default, so the exchange (RCCL / copies) is ordered with the
+        # kernels; its handle may be 0 (the null stream), hence FLAG_USE_STREAM
+        flags = (_abi.FLAG_KERNEL_TIMING if kernel_timing else 0) | _abi.FLAG_USE_STREAM
+        if stream is None:
+            stream = torch.cuda.current_stream(device).cuda_stream
+        self.cfg = _abi.Config(n_arg, _abi.TOPOLOGIES[topology], _abi.ALGOS[algorithm], seed, delta,
+                               gossip_threshold, term_init, term_limit, device, flags, 0, stream)
+        self.layout = _abi.Layout()
+        self.shard = _abi.ShardLayout()
+        h = C.c_void_p()
+        _abi.check(self.lib.gp_create_shard(C.byref(self.cfg), rank, world, C.byref(self.layout),
+                                            C.byref(self.shard), C.byref(h)))
+        self.h = h
+        self.rank, self.world = rank, world
+        self.topology, self.algorithm = topology, algorithm
+        self.lo, self.hi = int(self.shard.lo), int(self.shard.hi)
+        sb = np.zeros(world, np.int64)
+        rb = np.zeros(world, np.int64)
+        _abi.check(self.lib.gp_shard_plan(self.h, sb.ctypes.data_as(C.c_void_p), rb.ctypes.data_as(C.c_void_p)))
+        self.send_splits, self.recv_splits = [int(x) for x in sb], [int(x) for x in rb]
+        dev = torch.device("cuda", device)
+        # the caching allocator hands out 512-byte aligned blocks (the ABI needs 256)
+        self.send_buf = torch.zeros(max(1, int(sb.sum())), dtype=torch.uint8, device=dev)[: int(sb.sum())]
+        self.recv_buf = torch.zeros(max(1, int(rb.sum())), dtype=torch.uint8, device=dev)[: int(rb.sum())]
+        self.status = _abi.Status()
+
+    @property
+    def nodes(self) -> int:
+        return int(self.layout.nodes)
+
+    @property
+    def actors(self) -> int:
+        return int(self.layout.actors)
+
+    def round(self):
+        _abi.check(self.lib.gp_shard_round(self.h, C.c_void_p(self.send_buf.data_ptr())))
+
+    def deliver(self):
+        _abi.check(self.lib.gp_shard_deliver(self.h, C.c_void_p(self.recv_buf.data_ptr())))
+
+    def sync(self):
+        _abi.check(self.lib.gp_shard_sync(self.h, C.byref(self.status)))
+        return self.status
+
+    def reset(self):
+        _abi.check(self.lib.gp_reset(self.h))
+        self.status = _abi.Status()
+
+    # read-back of this rank's actors [lo, hi) (global ids)
+    def read_gossip(self):
+        n = self.hi - self.lo
+        cnt = np.zeros(n, np.uint32)
+        flags = np.zeros(n, np.uint8)
+        _abi.check(self.lib.gp_read_gossip(self.h, self.lo, n, cnt.ctypes.data_as(C.c_void_p),
+                                           flags.ctypes.data_as(C.c_void_p)))
+        return cnt, flags
+
+    def read_pushsum(self):
+        n = self.hi - self.lo
+        S = np.zeros(n, np.float64)
+        W = np.zeros(n, np.float64)
+        flags = np.zeros(n, np.uint8)
+        _abi.check(self.lib.gp_read_pushsum(self.h, self.lo, n, S.ctypes.data_as(C.c_void_p),
+                                            W.ctypes.data_as(C.c_void_p), flags.ctypes.data_as(C.c_void_p)))
+        return S, W, flags
+
+    def read_messages(self):
+        """Push-sum messages this rank's actors emitted in the last round: dst, s, w."""
+        n = self.hi - self.lo
+        d = np.zeros(n, np.uint32)
+        s = np.zeros(n, np.float64)
+        w = np.zeros(n, np.float64)
+        _abi.check(self.lib.gp_read_messages(self.h, self.lo, n, d.ctypes.data_as(C.c_void_p),
+                                             s.ctypes.data_as(C.c_void_p), w.ctypes.data_as(C.c_void_p)))
+        return d, s, w
+
+    def read_trace(self):
+        r = int(self.status.round)
+        out = np.zeros(r, np.int64)
+        if r:
+            _abi.check(self.lib.gp_read_trace(self.h, 0, r, out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def kernel_stats(self, reset: bool = False):
+        ks = _abi.KStats()
+        _abi.check(self.lib.gp_kernel_stats(self.h, C.byref(ks), 1 if reset else 0))
+        return {"launches": ks.launches, "total_ms": ks.total_ms, "avg_ms": ks.avg_ms,
+                "bytes_per_launch": ks.bytes_per_launch, "kernel": ks.kernel.decode(),
+                "aux_avg_ms": ks.aux_avg_ms, "aux_kernel": ks.aux_kernel.decode()}
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class TorchTransport:
+    """The per-round exchange as one torch.distributed all_to_all_single: RCCL over xGMI for
+    device buffers (backend "nccl" on ROCm), gloo for CPU buffers.  Sizes never change, so
+    there is no count exchange and no host synchronisation inside a round."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+
+    def exchange(self, eng):
+        self.dist.all_to_all_single(eng.recv_buf, eng.send_buf, eng.recv_splits, eng.send_splits,
+                                    group=self.group)
+
+
+def _offsets(splits):
+    return np.concatenate([[0], np.cumsum(splits)]).astype(np.int64)
+
+
+class LoopbackTransport:
+    """All shards live in this process (one GPU, or CPU): chunk p->q is copied from p's send
+    buffer into q's receive buffer (stream-ordered device copies for HipShard)."""
+
+    def exchange_all(self, engines):
+        so = [_offsets(e.send_splits) for e in engines]
+        ro = [_offsets(e.recv_splits) for e in engines]
+        for p, ep in enumerate(engines):
+            for q, eq in enumerate(engines):
+                n = ep.send_splits[q]
+                if p == q or n == 0:
+                    continue
+                assert n == eq.recv_splits[p], (p, q, n, eq.recv_splits[p])
+                eq.recv_buf[ro[q][p]:ro[q][p] + n].copy_(ep.send_buf[so[p][q]:so[p][q] + n])
+
+
+def run(engine, transport, max_rounds: int = 1 << 40, batch: int = 8, max_batch: int = 64):
+    """Advance this rank until the GLOBAL count reaches `nodes` (program.fs:49,56) or
+    max_rounds rounds; every rank of the job must call it with the same arguments."""
+    st = engine.sync()
+    goal = int(st.round) + max_rounds
+    while not st.converged and st.round < goal:
+        # gossip's F(k) reports round k-1, so one more exchange than rounds is needed to learn
+        # a convergence; rounds issued beyond it are no-ops on the device (gated).
+        b = min(batch, goal - int(st.round))
+        for _ in range(b):
+            engine.round()
+            transport.exchange(engine)
+            engine.deliver()
+        st = engine.sync()
+        batch = min(batch * 2, max_batch)
+    return st
+
+
+def run_local(engines, max_rounds: int = 1 << 40, batch: int = 8, max_batch: int = 64):
+    """`run` for every shard of a job held in this process (LoopbackTransport)."""
+    t = LoopbackTransport()
+    sts = [e.sync() for e in engines]
+    goal = int(sts[0].round) + max_rounds
+    while not sts[0].converged and sts[0].round < goal:
+        b = min(batch, goal - int(sts[0].round))
+        for _ in range(b):
+            for e in engines:
+                e.round()
+            t.exchange_all(engines)
+            for e in engines:
+                e.deliver()
+        sts = [e.sync() for e in engines]
+        assert len({(int(s.round), int(s.completed), int(s.converged)) for s in sts}) == 1, "shards disagree"
+        batch = min(batch * 2, max_batch)
+    return sts

@@ -36,6 +36,8 @@ class Simulator:
             raise ValueError("Invalid:Please enter a proper protocol or topology")
         self.lib = _abi.load()
         flags = (_abi.FLAG_KERNEL_TIMING if kernel_timing else 0) | (_abi.FLAG_GENERIC if generic else 0)
+        if stream is not None:  # an explicit stream, possibly 0 (the null stream)
+            flags |= _abi.FLAG_USE_STREAM
         self.cfg = _abi.Config(n_arg, _abi.TOPOLOGIES[topology], _abi.ALGOS[algorithm], seed, delta,
                                gossip_threshold, term_init, term_limit, device, flags, 0, stream)
         self.layout = _abi.Layout()
@@ -120,7 +122,8 @@ class Simulator:
         ks = _abi.KStats()
         _abi.check(self.lib.gp_kernel_stats(self.h, C.byref(ks), 1 if reset else 0))
         return {"launches": ks.launches, "total_ms": ks.total_ms, "avg_ms": ks.avg_ms,
-                "bytes_per_launch": ks.bytes_per_launch, "kernel": ks.kernel.decode()}
+                "bytes_per_launch": ks.bytes_per_launch, "kernel": ks.kernel.decode(),
+                "aux_avg_ms": ks.aux_avg_ms, "aux_kernel": ks.aux_kernel.decode()}
 
     def close(self):
         if getattr(self, "h", None):

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 1
+#define GP_ABI_VERSION 2
 
 /* program.fs:151 "line", :191 "full", :227 "2D", :267 "Imp3D"; "3D" is build-defined (Q9) */
 enum gp_topology { GP_LINE = 0, GP_FULL = 1, GP_TWO_D = 2, GP_IMP3D = 3, GP_THREE_D = 4 };
@@ -38,11 +38,13 @@ enum gp_error {
     GP_ENOMEM = -2, /* device or host allocation failed                  */
     GP_EHIP = -3,   /* a HIP runtime call failed                         */
     GP_ESTATE = -4, /* call not valid in the handle's current state      */
+    GP_EOVERFLOW = -5, /* a shard's fixed-capacity message buffer overflowed (results void) */
 };
 
 enum gp_flags {
     GP_FLAG_KERNEL_TIMING = 1, /* bracket every round kernel with hipEvents (gp_kernel_stats) */
     GP_FLAG_GENERIC = 2,       /* force the generic bucketed push path on grid topologies    */
+    GP_FLAG_USE_STREAM = 4,    /* run on cfg->stream even when it is NULL (the null stream)  */
 };
 
 typedef struct gp_config {
@@ -57,7 +59,8 @@ typedef struct gp_config {
     int32_t device;           /* HIP device ordinal                                     */
     int32_t flags;            /* gp_flags                                               */
     int32_t reserved;
-    void* stream;             /* optional hipStream_t to run on (NULL: library-owned)   */
+    void* stream;             /* hipStream_t to run on; NULL without GP_FLAG_USE_STREAM:
+                                 a library-owned stream                                  */
 } gp_config;
 
 typedef struct gp_layout {
@@ -81,11 +84,13 @@ typedef struct gp_status {
 } gp_status;
 
 typedef struct gp_kstats {
-    int64_t launches;   /* round kernels timed since the last reset                         */
-    double total_ms;    /* summed kernel durations                                         */
+    int64_t launches;   /* rounds timed since the last reset                               */
+    double total_ms;    /* summed durations of the dominant round kernel                   */
     double avg_ms;      /* total_ms / launches                                             */
-    double bytes_per_launch; /* algorithmic HBM bytes of one round kernel    */
+    double bytes_per_launch; /* compulsory HBM bytes of one launch of it     */
     char kernel[64];    /* name of the dominant round kernel                               */
+    double aux_avg_ms;  /* the pass that completes a round after it (0 if none)            */
+    char aux_kernel[64];
 } gp_kstats;
 
 int gp_abi_version(void);
@@ -119,6 +124,45 @@ int gp_neighbors(void* handle, int64_t v, uint32_t* out, int32_t cap);
 
 /* Per-kernel timing collected under GP_FLAG_KERNEL_TIMING; reset=1 clears the counters. */
 int gp_kernel_stats(void* handle, gp_kstats* out, int32_t reset);
+
+/* ---------------------------------------------------------------- node-range shards
+ * Multi-GPU: one process per GPU, each owning a contiguous actor range of the
+ * same global graph.  The reference has no counterpart (its only parallelism is the Akka
+ * dispatcher over the .NET thread pool, program.fs:23); these entry points split gp_step
+ * (program.fs:82-146 + :44-63) into the per-round pieces around ONE exchange, which the
+ * caller performs with any all-to-all (RCCL via torch.distributed on MI355X, gloo on CPU, a
+ * device copy for in-process shards).  Every buffer size is fixed at creation, so the
+ * exchange needs no per-round size negotiation and the round loop never waits on the host.
+ *
+ * Per round k:  gp_shard_round(send)  -> caller all-to-all(send -> recv) -> gp_shard_deliver(recv)
+ * and every few rounds gp_shard_sync() to learn the global completion count. */
+
+/* Actor range of every rank: bounds[0] = 0 < ... < bounds[world] = actors.  Grid topologies
+ * (Imp3D/3D) split on whole z-planes (G*G actors); line/2D/full split evenly. */
+int gp_partition(int64_t n_arg, int32_t topology, int32_t world, int64_t* bounds);
+
+typedef struct gp_shard_layout {
+    int64_t lo, hi;         /* this rank's actors [lo, hi)                                   */
+    int64_t halo;           /* actors exchanged with each z-neighbour rank per round (0: none) */
+    int64_t send_total;     /* bytes of the send buffer (sum of send_bytes)                  */
+    int64_t recv_total;     /* bytes of the receive buffer                                   */
+} gp_shard_layout;
+
+/* Create rank `rank` of `world` (cfg->device is this rank's GPU).  Supported: gossip on every
+ * topology, push-sum on line/2D/Imp3D/3D (push-sum on "full" is single-GPU only). */
+int gp_create_shard(const gp_config* cfg, int32_t rank, int32_t world, gp_layout* out,
+                    gp_shard_layout* shard, void** handle);
+/* Per-peer byte counts of the send and receive buffers (arrays of `world`; peer order). */
+int gp_shard_plan(void* handle, int64_t* send_bytes, int64_t* recv_bytes);
+/* Enqueue one round on the handle's stream and pack what other ranks need into send_buf
+ * (device memory, send_total bytes, 256-byte aligned).  Asynchronous. */
+int gp_shard_round(void* handle, void* send_buf);
+/* Enqueue the unpacking of what the other ranks sent for that round (recv_buf: recv_total
+ * bytes of device memory).  Must follow each gp_shard_round.  Asynchronous. */
+int gp_shard_deliver(void* handle, const void* recv_buf);
+/* Wait for the enqueued rounds and fill st from the global completion counts (st->sum_s /
+ * sum_w are this rank's share).  Fails with GP_EOVERFLOW if a link buffer overflowed. */
+int gp_shard_sync(void* handle, gp_status* st);
 
 void gp_destroy(void* handle);
 

@@ -112,6 +112,12 @@ typedef struct {
     double *S, *W, *Sin, *Win, *NSin, *NWin, *ms, *mw;
     uint32_t *cin, *Ncin, *tgt;
     uint8_t *term, *conv;
+    /* shard mode */
+    int shard, rank, world;
+    int64_t lo, hi, bnd[17];
+    int64_t calls;        /* gpo_shard_round calls so far                    */
+    int64_t own_newly;    /* this rank's count of the round being exchanged   */
+    int stopped;          /* global count reached nodes: later rounds are no-ops */
 } oracle_t;
 
 static int64_t deg_of(const oracle_t* o, int64_t v) {
@@ -489,5 +495,179 @@ int gpo_read_trace(void* h, int64_t first_round, int64_t count, int64_t* complet
     oracle_t* o = (oracle_t*)h;
     if (!o || first_round < 0 || count < 0 || first_round + count > o->round) return -1;
     memcpy(completed, o->trace + first_round, (size_t)count * sizeof(int64_t));
+    return 0;
+}
+
+/* ------------------------------------------------------------------ shard mode */
+typedef struct { int64_t newly, count; } shard_hdr;              /* 16 bytes */
+typedef struct { uint32_t src, dst; double s, w; } shard_msg;    /* 24 bytes */
+
+static int owner_of(const oracle_t* o, int64_t v) {
+    int q = 0;
+    while (q + 1 < o->world && v >= o->bnd[q + 1]) ++q;
+    return q;
+}
+
+/* Chunk from rank p: header + room for every message p's actors can emit in one round
+ * (push-sum: one per actor; gossip: one per activation chain, at most two per actor). */
+static int64_t chunk_bytes(const oracle_t* o, int p) {
+    const int64_t n = o->bnd[p + 1] - o->bnd[p];
+    return (int64_t)sizeof(shard_hdr) + (o->cfg.algo == GPO_GOSSIP ? 2 : 1) * n * (int64_t)sizeof(shard_msg);
+}
+
+void* gpo_shard_create(const gpo_config* cfg, int32_t rank, int32_t world, const int64_t* bounds, gpo_layout* out) {
+    if (world < 1 || world > 16 || rank < 0 || rank >= world || !bounds) return NULL;
+    oracle_t* o = (oracle_t*)gpo_create(cfg, out);
+    if (!o) return NULL;
+    if (bounds[0] != 0 || bounds[world] != o->A) { gpo_destroy(o); return NULL; }
+    for (int q = 0; q < world; ++q)
+        if (bounds[q + 1] <= bounds[q]) { gpo_destroy(o); return NULL; }
+    o->shard = 1;
+    o->rank = rank;
+    o->world = world;
+    for (int q = 0; q <= world; ++q) o->bnd[q] = bounds[q];
+    o->lo = bounds[rank];
+    o->hi = bounds[rank + 1];
+    return o;
+}
+
+int gpo_shard_plan(void* h, int64_t* send_bytes, int64_t* recv_bytes) {
+    oracle_t* o = (oracle_t*)h;
+    if (!o || !o->shard) return -1;
+    for (int q = 0; q < o->world; ++q) {
+        send_bytes[q] = q == o->rank ? 0 : chunk_bytes(o, o->rank);
+        recv_bytes[q] = q == o->rank ? 0 : chunk_bytes(o, q);
+    }
+    return 0;
+}
+
+static char* chunk_at(const oracle_t* o, char* base, int peer, int sending) {
+    int64_t off = 0;
+    for (int q = 0; q < peer; ++q)
+        if (q != o->rank) off += chunk_bytes(o, sending ? o->rank : q);
+    return base + off;
+}
+
+static void put_msg(oracle_t* o, char* send, uint32_t u, uint32_t t, double s, double w) {
+    const int q = owner_of(o, t);
+    shard_hdr* hd = (shard_hdr*)chunk_at(o, send, q, 1);
+    shard_msg* m = (shard_msg*)(hd + 1) + hd->count++;
+    m->src = u; m->dst = t; m->s = s; m->w = w;
+}
+
+/* Apply the receipts gathered for round a (program.fs:97-105) on this rank's actors. */
+static int64_t gossip_apply_own(oracle_t* o) {
+    const uint32_t thr = (uint32_t)o->cfg.gossip_threshold;
+    int64_t newly = 0;
+    for (int64_t v = o->lo; v < o->hi; ++v) {
+        uint32_t c0 = o->cnt[v], c1 = c0 + o->inc[v];
+        o->inc[v] = 0;
+        o->cnt[v] = c1;
+        if (c0 == 0 && c1 > 0) o->tok[v]++;
+        if (c0 <= thr && c1 >= thr + 1) { o->done[v] = 1; newly++; }
+    }
+    return newly;
+}
+
+int gpo_shard_round(void* h, void* send) {
+    oracle_t* o = (oracle_t*)h;
+    if (!o || !o->shard) return -1;
+    const uint32_t r = (uint32_t)o->calls;
+    for (int q = 0; q < o->world; ++q)
+        if (q != o->rank) { shard_hdr* hd = (shard_hdr*)chunk_at(o, (char*)send, q, 1); hd->newly = 0; hd->count = 0; }
+    int64_t newly = 0;
+    if (!o->stopped) {
+        if (o->cfg.algo == GPO_GOSSIP) {
+            /* the receipts of round r-1 are applied first (their count travels now), then the
+             * chains of round r draw; local receipts are filtered by done at round start */
+            if (r >= 1) newly = gossip_apply_own(o);
+            for (int64_t v = o->lo; v < o->hi; ++v) {
+                const int64_t d = deg_of(o, v);
+                for (int k = 0; k < o->tok[v] && d > 0; ++k) {
+                    uint32_t t = nbr_of(o, v, draw(o->cfg.seed, ST_GOSSIP, r, (uint32_t)v, k, (uint32_t)d));
+                    if (t >= o->lo && t < o->hi) { if (!o->done[t]) o->inc[t]++; }
+                    else put_msg(o, (char*)send, (uint32_t)v, t, 0.0, 0.0);
+                }
+            }
+        } else {
+            for (int64_t v = o->lo; v < o->hi; ++v) {
+                newly += ps_phase1(o, v, r);
+                const uint32_t t = o->tgt[v];
+                if (t != 0xFFFFFFFFu && (t < o->lo || t >= o->hi)) put_msg(o, (char*)send, (uint32_t)v, t, o->ms[v], o->mw[v]);
+            }
+        }
+    }
+    for (int q = 0; q < o->world; ++q)
+        if (q != o->rank) ((shard_hdr*)chunk_at(o, (char*)send, q, 1))->newly = newly;
+    o->own_newly = newly;
+    o->calls++;
+    return 0;
+}
+
+int gpo_shard_deliver(void* h, const void* recv) {
+    oracle_t* o = (oracle_t*)h;
+    if (!o || !o->shard || o->calls == 0) return -1;
+    const int64_t k = o->calls - 1;
+    int64_t newly = o->own_newly;
+    for (int q = 0; q < o->world; ++q)
+        if (q != o->rank) newly += ((const shard_hdr*)chunk_at(o, (char*)recv, q, 0))->newly;
+    if (!o->stopped) {
+        if (o->cfg.algo == GPO_GOSSIP) {
+            for (int q = 0; q < o->world; ++q) {
+                if (q == o->rank) continue;
+                const shard_hdr* hd = (const shard_hdr*)chunk_at(o, (char*)recv, q, 0);
+                const shard_msg* m = (const shard_msg*)(hd + 1);
+                for (int64_t i = 0; i < hd->count; ++i)
+                    if (!o->done[m[i].dst]) o->inc[m[i].dst]++;
+            }
+        } else {
+            /* inbox sums from +0.0 in ascending source order: ranks in order, own in place */
+            for (int64_t v = o->lo; v < o->hi; ++v) { o->NSin[v] = 0.0; o->NWin[v] = 0.0; o->Ncin[v] = 0; }
+            for (int q = 0; q < o->world; ++q) {
+                if (q == o->rank) {
+                    for (int64_t u = o->lo; u < o->hi; ++u) {
+                        const uint32_t t = o->tgt[u];
+                        if (t == 0xFFFFFFFFu || t < o->lo || t >= o->hi) continue;
+                        o->NSin[t] += o->ms[u]; o->NWin[t] += o->mw[u]; o->Ncin[t]++;
+                    }
+                    continue;
+                }
+                const shard_hdr* hd = (const shard_hdr*)chunk_at(o, (char*)recv, q, 0);
+                const shard_msg* m = (const shard_msg*)(hd + 1);
+                for (int64_t i = 0; i < hd->count; ++i) {
+                    o->NSin[m[i].dst] += m[i].s; o->NWin[m[i].dst] += m[i].w; o->Ncin[m[i].dst]++;
+                }
+            }
+            double* t;
+            t = o->Sin; o->Sin = o->NSin; o->NSin = t;
+            t = o->Win; o->Win = o->NWin; o->NWin = t;
+            uint32_t* tc = o->cin; o->cin = o->Ncin; o->Ncin = tc;
+        }
+        const int64_t applied = o->cfg.algo == GPO_GOSSIP ? k - 1 : k;
+        if (applied >= 0) {
+            o->completed += newly;
+            push_trace(o, o->round, o->completed);
+            o->round++;
+            if (o->completed >= o->lay.nodes) { o->converged = 1; o->stopped = 1; }
+        }
+    }
+    return 0;
+}
+
+int gpo_shard_sync(void* h, gpo_status* st) {
+    oracle_t* o = (oracle_t*)h;
+    if (!o || !o->shard) return -1;
+    st->round = o->round;
+    st->completed = o->completed;
+    st->converged = o->converged;
+    st->pad = 0;
+    st->sum_s = st->sum_w = 0.0;
+    if (o->cfg.algo == GPO_PUSHSUM) {
+        /* this rank's held mass plus what its actors sent in the last round */
+        for (int64_t v = o->lo; v < o->hi; ++v) {
+            if (deg_of(o, v) > 0) { st->sum_s += o->S[v]; st->sum_w += o->W[v]; }
+            if (o->calls > 0 && o->tgt[v] != 0xFFFFFFFFu) { st->sum_s += o->ms[v]; st->sum_w += o->mw[v]; }
+        }
+    }
     return 0;
 }

@@ -68,6 +68,19 @@ int  gpo_read_messages(void* h, int64_t first, int64_t count, uint32_t* dst, dou
 int  gpo_read_trace(void* h, int64_t first_round, int64_t count, int64_t* completed);
 void gpo_destroy(void* h);
 
+/* Shard mode (checker for the multi-GPU decomposition): rank `rank` of
+ * `world` owns actors [bounds[rank], bounds[rank+1]) of the same global graph.  Independent of
+ * the product's halo/slot scheme: every message whose destination belongs to another rank is
+ * shipped as an explicit (source, destination, s, w) record, and the receiver merges the
+ * records of all ranks in rank order — i.e. ascending source order, the canonical inbox order.
+ * Completion counts travel in each chunk's header.  Per round: gpo_shard_round(send) ->
+ * any all-to-all -> gpo_shard_deliver(recv); gpo_shard_sync reports the global count. */
+void* gpo_shard_create(const gpo_config* cfg, int32_t rank, int32_t world, const int64_t* bounds, gpo_layout* out);
+int  gpo_shard_plan(void* h, int64_t* send_bytes, int64_t* recv_bytes);
+int  gpo_shard_round(void* h, void* send);
+int  gpo_shard_deliver(void* h, const void* recv);
+int  gpo_shard_sync(void* h, gpo_status* st);
+
 #ifdef __cplusplus
 }
 #endif

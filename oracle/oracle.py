@@ -61,6 +61,12 @@ def lib():
         L.gpo_destroy.argtypes = [P]
         L.gpo_sizes.argtypes = [C.c_int64, C.c_int32, P, P, P]
         L.gpo_philox4x32_10.argtypes = [P, P, P]
+        L.gpo_shard_create.restype = P
+        L.gpo_shard_create.argtypes = [C.POINTER(Config), C.c_int32, C.c_int32, P, C.POINTER(Layout)]
+        L.gpo_shard_plan.argtypes = [P, P, P]
+        L.gpo_shard_round.argtypes = [P, P]
+        L.gpo_shard_deliver.argtypes = [P, P]
+        L.gpo_shard_sync.argtypes = [P, C.POINTER(Status)]
         _lib = L
     return _lib
 
@@ -163,3 +169,59 @@ class OracleSim:
             self.close()
         except Exception:
             pass
+
+
+class OracleShard(OracleSim):
+    """Rank `rank` of a sharded CPU run (gpo_shard_*): the checker of the multi-GPU
+    decomposition.  Same engine interface as gossip_amd.sharded.HipShard (round / deliver /
+    sync, send_buf / recv_buf with per-peer splits), with CPU torch tensors as buffers, so
+    the product's host loop and torch.distributed transport drive it unchanged (gloo)."""
+
+    def __init__(self, n_arg, topology, algo, *, rank, world, bounds, seed=1, **kw):
+        import torch
+
+        t = TOPOLOGIES[topology] if isinstance(topology, str) else topology
+        a = ALGOS[algo] if isinstance(algo, str) else algo
+        self.cfg = Config(n_arg, t, a, seed, kw.get("delta", 1e-10), kw.get("gossip_threshold", 10),
+                          kw.get("term_init", 1), kw.get("term_limit", 3))
+        self.layout = Layout()
+        self.algo = a
+        b = np.asarray(bounds, np.int64)
+        h = lib().gpo_shard_create(C.byref(self.cfg), rank, world, _ptr(b), C.byref(self.layout))
+        if not h:
+            raise ValueError(f"gpo_shard_create failed for {n_arg} {topology} {algo} rank {rank}/{world}")
+        self.h = C.c_void_p(h)
+        self.status = Status()
+        self.rank, self.world = rank, world
+        self.lo, self.hi = int(b[rank]), int(b[rank + 1])
+        sb = np.zeros(world, np.int64)
+        rb = np.zeros(world, np.int64)
+        lib().gpo_shard_plan(self.h, _ptr(sb), _ptr(rb))
+        self.send_splits, self.recv_splits = [int(x) for x in sb], [int(x) for x in rb]
+        self.send_buf = torch.zeros(int(sb.sum()), dtype=torch.uint8)
+        self.recv_buf = torch.zeros(int(rb.sum()), dtype=torch.uint8)
+
+    def round(self):
+        if lib().gpo_shard_round(self.h, C.c_void_p(self.send_buf.data_ptr())):
+            raise RuntimeError("gpo_shard_round")
+
+    def deliver(self):
+        if lib().gpo_shard_deliver(self.h, C.c_void_p(self.recv_buf.data_ptr())):
+            raise RuntimeError("gpo_shard_deliver")
+
+    def sync(self):
+        if lib().gpo_shard_sync(self.h, C.byref(self.status)):
+            raise RuntimeError("gpo_shard_sync")
+        return self.status
+
+    def _own(self, arrays):
+        return tuple(a[self.lo:self.hi] for a in arrays)
+
+    def read_gossip(self):
+        return self._own(super().read_gossip())
+
+    def read_pushsum(self):
+        return self._own(super().read_pushsum())
+
+    def read_messages(self):
+        return self._own(super().read_messages())

@@ -1,0 +1,134 @@
+"""Multi-rank path on CPU: the product's shard host loop (gossip_amd.sharded.run) and its
+torch.distributed transport, over gloo with world_size 2 and 3, driving the CPU oracle's shard
+engine (oracle.OracleShard).  Each rank owns the node range gp_partition gives it (whole
+z-planes for Imp3D/3D); the job must reproduce the single-process oracle bit for bit —
+completion trace, convergence round and every actor's state."""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CASES = [
+    # (n_arg, topology, algorithm, seed, round cap)
+    (1000, "Imp3D", "push-sum", 1, 4000),
+    (200, "3D", "push-sum", 3, 4000),
+    (200, "line", "push-sum", 2, 300),
+    (50, "2D", "push-sum", 3, 400),
+    (1000, "full", "gossip", 1, 4000),
+    (1000, "Imp3D", "gossip", 3, 4000),
+    (200, "line", "gossip", 3, 20000),
+    (64, "2D", "gossip", 2, 20000),
+    (200, "3D", "gossip", 1, 4000),
+]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, case, bounds, q):
+    for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "cop5615-gossip_protocol_amd")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import oracle
+    from gossip_amd import sharded
+
+    n, topo, algo, seed, cap = case
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        eng = oracle.OracleShard(n, topo, algo, rank=rank, world=world, bounds=bounds, seed=seed)
+        st = sharded.run(eng, sharded.TorchTransport(), max_rounds=cap)
+        state = eng.read_gossip() if algo == "gossip" else eng.read_pushsum()
+        sums = None
+        if algo == "push-sum":  # global mass = sum over ranks of held + in-flight
+            import torch
+            t = torch.tensor([st.sum_s, st.sum_w], dtype=torch.float64)
+            dist.all_reduce(t)
+            sums = t.tolist()
+        q.put((rank, int(st.round), int(st.completed), int(st.converged), eng.read_trace(),
+               [np.asarray(a) for a in state], sums))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_job(case, world, bounds):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, bounds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(out, key=lambda x: x[0])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[2]}-{c[1]}-{c[0]}")
+def test_sharded_matches_single_process(case, world):
+    import oracle
+    from gossip_amd import sharded
+
+    n, topo, algo, seed, cap = case
+    bounds = sharded.partition(n, topo, world)
+    ref = oracle.OracleSim(n, topo, algo, seed=seed)
+    rs = ref.step(cap)
+    ref_state = ref.read_gossip() if algo == "gossip" else ref.read_pushsum()
+    ref_trace = ref.read_trace()
+    out = _run_job(case, world, bounds)
+    for rank, rnd, comp, conv, trace, state, sums in out:
+        assert (rnd, comp, conv) == (rs.round, rs.completed, rs.converged), (rank, rnd, rs.round)
+        np.testing.assert_array_equal(trace, ref_trace)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        for got, want in zip(state, ref_state):
+            np.testing.assert_array_equal(got, want[lo:hi])  # bit-exact, fp64 included
+        if sums is not None:  # conservation: sum s = sum of ids, sum w = participants
+            assert sums[1] == pytest.approx(ref.layout.participants, rel=1e-12)
+            assert sums[0] == pytest.approx(rs.sum_s, rel=1e-12)
+    ref.close()
+
+
+def test_uneven_partition_gossip_full():
+    """Any contiguous split gives the same run (here not the gp_partition one)."""
+    import oracle
+
+    case = (300, "full", "gossip", 2, 4000)
+    bounds = [0, 17, 301]
+    ref = oracle.OracleSim(300, "full", "gossip", seed=2)
+    rs = ref.step(4000)
+    cnt, flags = ref.read_gossip()
+    out = _run_job(case, 2, bounds)
+    for rank, rnd, comp, conv, trace, state, _ in out:
+        assert (rnd, comp, conv) == (rs.round, rs.completed, rs.converged)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        np.testing.assert_array_equal(state[0], cnt[lo:hi])
+        np.testing.assert_array_equal(state[1], flags[lo:hi])
+
+
+def test_partition_rules():
+    from gossip_amd import sharded
+
+    # Imp3D 10M: nodes 9,938,375, G = 239, plane 57,121, 174 planes
+    b = sharded.partition(10_000_000, "Imp3D", 8)
+    assert b[0] == 0 and b[-1] == 9_938_376 and len(b) == 9
+    assert all(x % 57_121 == 0 for x in b[1:-1])
+    assert all(b[i] < b[i + 1] for i in range(8))
+    b = sharded.partition(1000, "line", 3)
+    assert b == [0, 333, 667, 1001]
+    from gossip_amd import GossipError
+    with pytest.raises(GossipError):
+        sharded.partition(20, "Imp3D", 8)  # 2 z-planes cannot feed 8 ranks
+    with pytest.raises(GossipError):
+        sharded.partition(1000, "Imp3D", 17)  # more ranks than the exchange supports
