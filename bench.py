@@ -2,14 +2,16 @@
 imperfect-3D, 10M nodes (configs[2]: `10000000 Imp3D push-sum`, 9,938,375 nodes, G = 239).
 
 One step = one complete simulation to convergence from the reference's initial state
-(S_i = i, W_i = 1, termRound = 1; program.fs:78-79,107-108): gp_reset + gp_step.  Topology
-build (extra links, link CSR) happens once before timing, as the reference starts its timer
-after building the actors (program.fs:317).
+(S_i = i, W_i = 1, termRound = 1; program.fs:78-79,107-108): reset + run.  Topology build
+(extra links, link CSR) happens once before timing, as the reference starts its timer after
+building the actors (program.fs:317).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n 10000000] [--no-cpu-baseline]
 
-For N > 1 it is launched by torch.distributed.run, one rank per GPU.
-Rank 0 prints ONE JSON line.
+N = 1: the single-GPU engine (gp_step).  N > 1 (launched by torch.distributed.run, one rank per
+GPU): ONE graph of N x 10M nodes (weak scaling) split into node-range shards (whole z-planes),
+one fixed-size RCCL all-to-all per round.  value = global actors x rounds /
+max-over-ranks wall time.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -26,6 +28,13 @@ METRIC = "node-updates/sec + wall-time to push-sum convergence, imperfect3D 10M 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+def survey_bytes_per_update(topology, algorithm):
+    """algorithmic HBM bytes per node-update (the roofline's unit)."""
+    if algorithm == "gossip":
+        return 19.0
+    return 112.0 if topology == "Imp3D" else 108.0
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -38,21 +47,27 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--engine", choices=["auto", "shard"], default="auto",
+                    help="auto: single-GPU engine at N=1, shards at N>1; shard: shards also at N=1")
     return ap.parse_args()
 
 
-def pmc_traffic(kernel: str, workload: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
+def pmc_traffic(kernels, workload: str):
+    """HBM bytes per round of `kernels` (summed) from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, made by tools/make_pmc_traffic.py), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    e = d.get(kernel)
-    if not e or e.get("workload") != workload:
-        return None
-    return e.get("hbm_bytes_per_launch")
+    total = 0.0
+    for k in kernels:
+        e = d.get(k)
+        if not e or e.get("workload") != workload:
+            return None
+        total += e["hbm_bytes_per_launch"]
+    return total
 
 
 def cpu_baseline(n, topology, algorithm, seed, budget_s):
@@ -83,6 +98,26 @@ def cpu_baseline(n, topology, algorithm, seed, budget_s):
                       f"({sim.actors} actors), oracle/gp_oracle.c OpenMP pull mode, {el:.1f} s"}
 
 
+def roofline(ks, bytes_per_update, actors, workload):
+    """Round roofline: SURVEY §8(d) bytes per node-update x this rank's actors over the
+    measured duration of one round = the round kernel + the pass that completes it (link
+    scatter), both timed with hipEvents on the engine's stream inside the timed steps."""
+    if not ks["launches"]:
+        return None
+    round_ms = ks["avg_ms"] + ks["aux_avg_ms"]
+    algo_bytes = bytes_per_update * actors
+    achieved = algo_bytes / (round_ms * 1e-3) / 1e9
+    kernels = [ks["kernel"]] + ([ks["aux_kernel"]] if ks["aux_kernel"] else [])
+    traffic = pmc_traffic(kernels, workload)
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": " + ".join(kernels), "avg_kernel_ms": round(ks["avg_ms"], 5),
+            "avg_aux_ms": round(ks["aux_avg_ms"], 5), "round_ms": round(round_ms, 5),
+            "bytes_per_launch": algo_bytes, "bytes_per_update": bytes_per_update, "launches": ks["launches"],
+            "layout_bytes_per_launch": ks["bytes_per_launch"],
+            "layout_frac": round(ks["bytes_per_launch"] / (ks["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def main():
     args = parse()
     import torch
@@ -91,30 +126,44 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_shards = world > 1 or args.engine == "shard"
+    if use_shards:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    from gossip_amd import Simulator
+    from gossip_amd import Simulator, sharded
 
-    stream = torch.cuda.Stream()
-    # N > 1: every rank simulates its own node range; see DESIGN.md §6 for the sharded engine
-    sim = Simulator(args.n, args.topology, args.algorithm, seed=args.seed + rank, device=local,
-                    kernel_timing=not args.no_kernel_timing, stream=stream.cuda_stream)
+    timing = not args.no_kernel_timing
+    n_arg = args.n * world  # weak scaling: ~args.n nodes per GPU
+    if use_shards:
+        eng = sharded.HipShard(n_arg, args.topology, args.algorithm, rank=rank, world=world, seed=args.seed,
+                               device=local, kernel_timing=timing)
+        transport = sharded.TorchTransport()
+        own = eng.hi - eng.lo
 
-    def one_step():
-        sim.reset()
-        st = sim.step()
-        return int(st.round), bool(st.converged)
+        def one_step():
+            eng.reset()
+            st = sharded.run(eng, transport)
+            return int(st.round), bool(st.converged)
+    else:
+        stream = torch.cuda.Stream()
+        eng = Simulator(n_arg, args.topology, args.algorithm, seed=args.seed, device=local,
+                        kernel_timing=timing, stream=stream.cuda_stream)
+        own = eng.actors
+
+        def one_step():
+            eng.reset()
+            st = eng.step()
+            return int(st.round), bool(st.converged)
 
     for _ in range(args.warmup):
         one_step()
-    sim.kernel_stats(reset=True)
+    eng.kernel_stats(reset=True)
 
     def barrier():
-        if world > 1:
+        if use_shards:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -122,40 +171,25 @@ def main():
     converged = True
     barrier()
     t0 = time.perf_counter()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
     for _ in range(args.steps):
         r, c = one_step()
         rounds_total += r
         converged &= c
-    ev1.record(stream)
     barrier()
     elapsed = time.perf_counter() - t0
-    gpu_ms = ev0.elapsed_time(ev1)
-    updates = float(sim.actors) * rounds_total
-    if world > 1:
+    updates = float(eng.actors) * rounds_total  # global actors: every rank agrees on the rounds
+    if use_shards:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        u = torch.tensor([updates], device="cuda", dtype=torch.float64)
-        dist.all_reduce(u, op=dist.ReduceOp.SUM)
-        updates = float(u.item())
-    ks = sim.kernel_stats()
-    workload = f"{args.n} {args.topology} {args.algorithm}"
+    ks = eng.kernel_stats()
+    workload = f"{n_arg} {args.topology} {args.algorithm}"
     out = None
     if rank == 0:
-        roofline = None
-        if ks["launches"]:
-            achieved = ks["bytes_per_launch"] / (ks["avg_ms"] * 1e-3) / 1e9
-            tr = pmc_traffic(ks["kernel"], workload)
-            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr,
-                        "kernel": ks["kernel"], "avg_kernel_ms": round(ks["avg_ms"], 5),
-                        "bytes_per_launch": ks["bytes_per_launch"], "launches": ks["launches"]}
+        roof = roofline(ks, survey_bytes_per_update(args.topology, args.algorithm), own, workload)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.n, args.topology, args.algorithm, args.seed, args.cpu_seconds)
+            cpu = cpu_baseline(n_arg, args.topology, args.algorithm, args.seed, args.cpu_seconds)
         rounds_per_step = rounds_total / max(1, args.steps)
         out = {
             "metric": METRIC,
@@ -170,17 +204,17 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (reference initial state S_i=i, W_i=1; Philox seed %d)" % args.seed,
-            "config": {"workload": workload, "actors_per_gpu": sim.actors, "nodes_per_gpu": sim.nodes,
-                       "grid": int(sim.layout.grid), "rounds_to_convergence": rounds_per_step,
-                       "converged": converged, "parallelism": f"dp{world}" if world > 1 else "single",
-                       "gpu_event_ms_per_step": gpu_ms / args.steps},
+            "config": {"workload": workload, "actors": eng.actors, "nodes": eng.nodes,
+                       "actors_per_gpu": own, "grid": int(eng.layout.grid),
+                       "rounds_to_convergence": rounds_per_step, "converged": converged,
+                       "parallelism": f"node-range shards x{world}, RCCL all-to-all" if use_shards else "single"},
             "wall_time_to_convergence_ms": elapsed * 1e3 / args.steps,
-            "roofline": roofline,
+            "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    sim.close()
-    if world > 1:
+    eng.close()
+    if use_shards:
         dist.destroy_process_group()
     return out
 
