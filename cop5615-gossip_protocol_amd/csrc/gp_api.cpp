@@ -112,7 +112,8 @@ struct Handle {
     uint32_t* rev_src = nullptr;
     uint32_t* lpos = nullptr;
     uint8_t* lcnt[2] = {nullptr, nullptr};   // gossip link slots
-    double2* lmsg[2] = {nullptr, nullptr};   // push-sum link slots
+    double2* lmsg[2] = {nullptr, nullptr};   // push-sum link slots (sharded: remote senders)
+    unsigned long long* lbits[2] = {nullptr, nullptr};  // push-sum link bitmap, bit v - lo
     // push-sum
     double2* msg[2] = {nullptr, nullptr};
     uint8_t* dir[2] = {nullptr, nullptr};
@@ -209,6 +210,8 @@ struct Handle {
         a.lcnt_cur = lcnt[c];
         a.lmsg_prev = lmsg[p];
         a.lmsg_cur = lmsg[c];
+        a.lbits_prev = lbits[p];
+        a.lbits_cur = lbits[c];
         a.msg_prev = msg[p];
         a.msg_cur = msg[c];
         a.dir_prev = dir[p];
@@ -278,8 +281,13 @@ int build_links(Handle* h) {
     if (!h->generic) {  // pull kernels: sender-pushed link slots
         if (h->gossip) {
             if ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))) return rc;
-        } else if ((rc = h->alloc(&h->lmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lmsg[1], (size_t)nsl, slo))) {
-            return rc;
+        } else {
+            // one bitmap word per 64 own actors (+1: the last wave may straddle hi)
+            const size_t words = ((size_t)h->own() + 63) / 64 + 1;
+            if ((rc = h->alloc(&h->lbits[0], words)) || (rc = h->alloc(&h->lbits[1], words))) return rc;
+            if (h->sharded &&
+                ((rc = h->alloc(&h->lmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lmsg[1], (size_t)nsl, slo))))
+                return rc;
         }
     }
     if (h->sharded) {  // link counts per (source rank, destination rank, sender degree)
@@ -385,21 +393,23 @@ int reset(Handle* h) {
 
 const char* round_kernel_name(const Handle* h) {
     if (h->gossip) return h->generic ? "k_gs_push" : (h->g.has_link ? "k_gs_pull<true>" : "k_gs_pull<false>");
-    return h->generic ? "k_ps_push_emit" : (h->g.has_link ? "k_ps_pull<true>" : "k_ps_pull<false>");
+    if (h->generic) return "k_ps_push_emit";
+    return !h->g.has_link ? "k_ps_pull<0>" : (h->sharded ? "k_ps_pull<2>" : "k_ps_pull<1>");
 }
 
 const char* aux_kernel_name(const Handle* h) {
     if (h->generic) return h->gossip ? "" : "k_scan_* + k_ps_push_fill";
     if (!h->g.has_link) return "";
-    return h->gossip ? "k_gs_link_scatter" : "k_ps_link_scatter";
+    if (h->gossip) return "k_gs_link_scatter";
+    return h->sharded ? "k_ps_link_scatter_x" : "";  // one GPU: the receiver gathers (no pass)
 }
 
 // Compulsory HBM bytes of one launch of the dominant round kernel for its data layout
 // (every array element it must touch, touched once); DESIGN.md §5.
 //   push-sum pull: held (S,W) read 16 + message write 16 + flags read 1 + direction byte read
 //   1 (own row; neighbour rows re-read from cache) + direction write 1 per participant; Imp3D
-//   adds the link CSR offsets (4 per actor) and per link slot the 16-byte slot + 4-byte source.
-//   The link scatter pass (a separate kernel) is not included.
+//   adds the link CSR offsets (4 per actor), the 4-byte source per link, one bitmap bit per
+//   actor, and the 16-byte message of every link that fired (~1 in 7: the interior degree).
 //   gossip pull: state byte read 1 + direction byte read 1 + write 1 (+ count r/w 8 on the
 //   receipts, not modelled); Imp3D adds offsets 4 per actor and 1 per link slot.
 double bytes_per_round(const Handle* h) {
@@ -411,7 +421,7 @@ double bytes_per_round(const Handle* h) {
     }
     if (h->generic) return P * (16 + 16 + 16 + 1 + 4 + 4 + 4 + 4 + 4);
     double b = P * (16 + 16 + 1 + 1 + 1);
-    if (h->g.has_link) b += 4 * A + links * (16 + 4);
+    if (h->g.has_link) b += 4 * A + links * 4 + A / 8 + links / 7 * 16;
     return b;
 }
 
@@ -447,9 +457,8 @@ void launch_aux(Handle* h, int64_t k, const Xchg* x) {
         const int c = (int)(r & 1u);
         launch_exclusive_scan(h->bcnt[c], h->boff[c], h->g.actors, h->scan_scratch, h->stream);
         launch_ps_push_fill(a, h->slot[c], h->boff[c], l);
-    } else if (h->g.has_link) {
-        if (x) launch_ps_link_scatter_x(a, *x, l);
-        else launch_ps_link_scatter(a, l);
+    } else if (h->g.has_link && x) {
+        launch_ps_link_scatter_x(a, *x, l);
     }
 }
 

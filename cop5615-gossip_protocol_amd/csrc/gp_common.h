@@ -45,6 +45,24 @@ __host__ __device__ __forceinline__ uint4 philox(uint32_t v, uint32_t r, uint32_
     return make_uint4(c0, c1, c2, c3);
 }
 
+// Word x of philox(); 32x32->64 products map to one v_mad_u64_u32 each on gfx950 (half the
+// multiply instructions of separate mul_hi / mul_lo), and the dead last-round words drop out.
+__host__ __device__ __forceinline__ uint32_t philox_x(uint32_t v, uint32_t r, uint32_t stream, uint64_t seed) {
+    uint32_t c0 = v, c1 = r, c2 = 0u, c3 = stream;
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint64_t p0 = (uint64_t)kPhiloxM0 * c0, p1 = (uint64_t)kPhiloxM1 * c2;
+        c0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        c1 = (uint32_t)p1;
+        c2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c3 = (uint32_t)p0;
+        k0 += kPhiloxW0;
+        k1 += kPhiloxW1;
+    }
+    return c0;
+}
+
 // Random().Next(0, n) replacement: floor(x * n / 2^32).
 __host__ __device__ __forceinline__ uint32_t scale_draw(uint32_t x, uint32_t n) { return mulhi32(x, n); }
 

@@ -11,7 +11,7 @@ constexpr int kPartStride = 16;     // u32 words between sub-counters
 constexpr int kPartRing = 4;        // rounds kept in the sub-counter ring
 // empty link slot: w holds this quiet-NaN bit pattern (a real weight is finite and >= 0)
 constexpr unsigned long long kEmptySlot = 0x7FF800000000DEADull;
-constexpr int kMaxWorld = 16;       // ranks of a sharded run (one per GPU; 8 on an MI355X node)
+constexpr int kMaxWorld = 16;
 
 // One synchronous round kernel F(r) fuses phase 2 of round r-1 (collect the messages sent to
 // this actor, read from the round r-1 buffers) with phase 1 of round r (update, convergence
@@ -39,13 +39,18 @@ struct RoundArgs {
     const uint32_t* rev_off;  // CSR of link sources per destination, ascending
     const uint32_t* rev_src;
     const uint32_t* lpos;     // CSR slot of v's own link edge: rev_src[lpos[v]] == v
-    // extra-link messages are PUSHED by the sender into its CSR slot (ping-pong); the receiver
-    // scans its slots in order and empties what it consumed (push-sum: w = kEmptySlot NaN;
-    // gossip: a u8 chain count set back to 0).
+    // Gossip: extra-link receipts are PUSHED by the sender into its CSR slot (ping-pong); the
+    // receiver scans its slots in order and empties what it consumed (a u8 chain count set back
+    // to 0).  Sharded push-sum slots hold (s, w), emptied with w = kEmptySlot NaN.
+    // Push-sum (k_ps_pull): the receiver reads a local sender's message from msg_prev after
+    // checking the sender's bit in the link bitmap (bit v - lo; ping-pong); only a sharded
+    // run's remote senders deliver through the CSR slots lmsg (written by the exchange).
     uint8_t* lcnt_prev;
     uint8_t* lcnt_cur;
     double2* lmsg_prev;
     double2* lmsg_cur;
+    const unsigned long long* lbits_prev;
+    unsigned long long* lbits_cur;
     // push-sum state
     const double2* msg_prev;  // message emitted in round r-1 (= held S,W when not converged)
     double2* msg_cur;
@@ -114,7 +119,6 @@ uint32_t span_for(uint32_t n, int grid);
 // round kernels
 void launch_ps_pull(const RoundArgs& a, const Launch& l);
 void launch_gs_pull(const RoundArgs& a, const Launch& l);
-void launch_ps_link_scatter(const RoundArgs& a, const Launch& l);
 void launch_gs_link_scatter(const RoundArgs& a, const Launch& l);
 void launch_ps_push_emit(const RoundArgs& a, const Launch& l);
 void launch_ps_push_fill(const RoundArgs& a, uint32_t* slot_cur, const uint32_t* boff_cur, const Launch& l);

@@ -147,12 +147,24 @@ __device__ __forceinline__ bool slot_full(double2 m) {
     return (unsigned long long)__double_as_longlong(m.y) != kEmptySlot;
 }
 
-// One actor's round.  All loads are unconditional (clamped addresses) and issued in two
-// dependency levels: (1) own flags + held (S,W), the six neighbours' direction bytes, the
-// link-slot range; (2) the grid messages that hit v and the first kLinkUnroll link slots
-// (each a 16-byte message written by its sender, or the empty marker) with their source
-// ids.  Consumed link slots are emptied for reuse two rounds later.
-template <bool LINK>
+// Link bitmap: bit (v - lo) is set iff actor v's round message took its extra link (direction
+// code 6).  One 64-bit word per wave, written by a ballot: a wave covers 64 consecutive actors
+// starting at a multiple of 64 from lo.
+__device__ __forceinline__ bool link_bit(const unsigned long long* bits, uint32_t off) {
+    return ((bits[off >> 6] >> (off & 63u)) & 1ull) != 0ull;
+}
+// One actor's round (program.fs:119-143 after collecting the round r-1 messages to v).
+// Collect = the canonical sequential fp64 sum, from +0.0, of the messages sent to v in ascending
+// source id.  Messages are never copied: a message IS the sender's held state, so a grid
+// sender's message is read from msg_prev at v-G^2, v-G, v-1, v+1, v+G or v+G^2 (a sender targets
+// v iff its direction byte is the opposite code), and an extra-link sender u (CSR rev_src,
+// ascending) from msg_prev[u] iff u's bit is set in the link bitmap.  Loads are unconditional
+// (clamped addresses) in four dependency levels: (1) own flags, held (S,W), the six neighbours'
+// direction bytes, the CSR range; (2) the first 3 grid hits' messages and the first kLinkUnroll
+// link sources; (3) those sources' bitmap words; (4) the fired links' messages.
+// LM: 0 no extra links; 1 links, every source local; 2 sharded: a source outside [lo, hi)
+// delivers through its CSR slot in lmsg_prev (written by the exchange), emptied after use.
+template <int LM>
 __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
     if (gate(a, a.r)) return;
     const Geom g = a.g;
@@ -162,13 +174,13 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
     uint32_t newly = 0;
     for (; v < end; v += step) {
         const uint32_t m = presence(g, v);
-        if (!m) continue;  // non-participant: never sends, never receives
+        bool linked = false;
+        if (m) {
         const uint32_t code = (a.ablate & 8u) ? kth_bit(m, v % popc(m))
-                                              : kth_bit(m, scale_draw(philox(v, r, kStreamPush, a.seed).x, popc(m)));
-        // ---- level 1
+                                              : kth_bit(m, scale_draw(philox_x(v, r, kStreamPush, a.seed), popc(m)));
         uint8_t f = a.flags[v];
-        double2 held = make_double2((double)v, 1.0);  // InitializeVariables (program.fs:107-108)
-        double ss = 0.0, ww = 0.0;  // inbox sum from +0.0 in ascending source order
+        double2 held = make_double2((double)v, 1.0);
+        double ss = 0.0, ww = 0.0;
         uint32_t cin = 0;
         if (r) {
             held = a.msg_prev[v];
@@ -176,7 +188,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
 #pragma unroll
             for (uint32_t k = 0; k < 6; ++k) d[k] = load_sel(a.dir_prev, (m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
             uint32_t li = 0, nl = 0;
-            if (LINK) {
+            if (LM) {
                 li = a.rev_off[v];
                 nl = (a.ablate & 1u) ? 0u : a.rev_off[v + 1] - li;
             }
@@ -184,8 +196,6 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
 #pragma unroll
             for (uint32_t k = 0; k < 6; ++k) hits |= ((m & slot_bit(k)) && d[k] == slot_code(k)) ? 1u << k : 0u;
             if (a.ablate & 16u) hits = 0;
-            // ---- level 2: the first three grid hits (Binomial(6, ~1/7): >99% of actors), in
-            // slot (= ascending source) order; more hits are picked up by the tail in flush()
             uint32_t hk[3], rest = hits;
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
@@ -195,13 +205,12 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
             double2 gm[3];
 #pragma unroll
             for (int j = 0; j < 3; ++j) gm[j] = load_sel(a.msg_prev, hk[j] < 6u, slot_src(g, v, hk[j] < 6u ? hk[j] : 0u), v);
-            uint32_t gi = 0;  // next grid hit to add (index into hk; >= 3 means the tail)
+            uint32_t gi = 0;
             auto add = [&](double2 mm) {
                 ss += mm.x;
                 ww += mm.y;
                 ++cin;
             };
-            // add pending grid messages from sources below `bound` (hits are ascending)
             auto flush = [&](uint32_t bound) {
 #pragma unroll
                 for (int j = 0; j < 3; ++j)
@@ -209,7 +218,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
                         add(gm[j]);
                         ++gi;
                     }
-                if (gi >= 3) {  // rare: a 4th+ grid hit (loaded on demand)
+                if (gi >= 3) {
                     while (rest) {
                         const uint32_t k = (uint32_t)__builtin_ctz(rest);
                         const uint32_t u = slot_src(g, v, k);
@@ -219,28 +228,52 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
                     }
                 }
             };
-            if (LINK) {
-                double2 lm[kLinkUnroll];
+            if (LM) {
                 uint32_t ls[kLinkUnroll];
 #pragma unroll
+                for (uint32_t k = 0; k < kLinkUnroll; ++k) ls[k] = load_sel(a.rev_src, k < nl, li + k, a.slot_lo);
+                // ---- level 3: the sources' link bits (a 1.2 MB bitmap at 10M actors: L2-resident);
+                // sharded: a remote source's CSR slot instead (filled by the exchange, emptied here)
+                bool lk[kLinkUnroll], loc[kLinkUnroll];
+                double2 lm[kLinkUnroll];
+#pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) {
-                    lm[k] = load_sel(a.lmsg_prev, k < nl, li + k, a.slot_lo);
-                    ls[k] = load_sel(a.rev_src, k < nl, li + k, a.slot_lo);
+                    const uint32_t off = ls[k] - a.lo;
+                    loc[k] = LM == 1 || off < a.hi - a.lo;
+                    const unsigned long long w = load_sel(a.lbits_prev, k < nl && loc[k], off >> 6, 0u);
+                    lk[k] = k < nl && loc[k] && ((w >> (off & 63u)) & 1ull);
+                    if (LM == 2) {
+                        lm[k] = load_sel(a.lmsg_prev, k < nl && !loc[k], li + k, a.slot_lo);
+                        if (k < nl && !loc[k] && slot_full(lm[k])) {
+                            lk[k] = true;
+                            a.lmsg_prev[li + k].y = __longlong_as_double((long long)kEmptySlot);
+                        }
+                    }
                 }
-                // merge: link slots are sorted by source; a sender matches grid OR link, never both
+                // ---- level 4: the messages of the local sources that took their link to v
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k)
-                    if (k < nl && slot_full(lm[k])) {
+                    if (loc[k]) lm[k] = load_sel(a.msg_prev, lk[k], ls[k], v);
+#pragma unroll
+                for (uint32_t k = 0; k < kLinkUnroll; ++k)
+                    if (lk[k]) {
                         flush(ls[k]);
                         add(lm[k]);
-                        a.lmsg_prev[li + k].y = __longlong_as_double((long long)kEmptySlot);
                     }
                 for (uint32_t k = kLinkUnroll; k < nl; ++k) {  // rare: more than kLinkUnroll sources
-                    const double2 mm = a.lmsg_prev[li + k];
-                    if (slot_full(mm)) {
-                        flush(a.rev_src[li + k]);
-                        add(mm);
-                        a.lmsg_prev[li + k].y = __longlong_as_double((long long)kEmptySlot);
+                    const uint32_t u = a.rev_src[li + k];
+                    if (LM == 1 || u - a.lo < a.hi - a.lo) {
+                        if (link_bit(a.lbits_prev, u - a.lo)) {
+                            flush(u);
+                            add(a.msg_prev[u]);
+                        }
+                    } else {
+                        const double2 mm = a.lmsg_prev[li + k];
+                        if (slot_full(mm)) {
+                            flush(u);
+                            add(mm);
+                            a.lmsg_prev[li + k].y = __longlong_as_double((long long)kEmptySlot);
+                        }
                     }
                 }
             }
@@ -248,12 +281,18 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
         }
         const uint8_t f0 = f;
         const PsOut o = ps_update(f, held, ss, ww, cin, a.delta, a.term_limit);
-        if (o.send) a.msg_cur[v] = o.msg;  // a link message is scattered by k_ps_link_scatter
+        if (o.send) a.msg_cur[v] = o.msg;
         a.dir_cur[v] = o.send ? (uint8_t)code : kDirNone;
+        linked = o.send && code == kDirLink;
         if (f != f0) a.flags[v] = f;
         if (o.conv_now) {
             a.frozen[v] = o.msg;
             ++newly;
+        }
+        }
+        if (LM) {
+            const unsigned long long bits = __ballot(linked);
+            if ((threadIdx.x & 63u) == 0u) a.lbits_cur[(v - a.lo) >> 6] = bits;
         }
     }
     block_add(newly, a.parts, r);
@@ -336,28 +375,6 @@ __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
 // (memory-level parallelism), then the scattered stores.
 constexpr uint32_t kScatterPer = 4;
 
-__global__ __launch_bounds__(kBlock) void k_ps_link_scatter(RoundArgs a) {
-    const uint32_t n = a.g.wired;
-    const uint32_t base = blockIdx.x * kBlock * kScatterPer + threadIdx.x;
-    bool l[kScatterPer];
-#pragma unroll
-    for (uint32_t j = 0; j < kScatterPer; ++j) {
-        const uint32_t u = base + j * kBlock;
-        l[j] = u < n && load_sel(a.dir_cur, u < n, u, 0u) == kDirLink;
-    }
-    uint32_t lp[kScatterPer];
-    double2 mm[kScatterPer];
-#pragma unroll
-    for (uint32_t j = 0; j < kScatterPer; ++j) {
-        const uint32_t u = base + j * kBlock;
-        lp[j] = load_sel(a.lpos, l[j], u, 0u);
-        mm[j] = load_sel(a.msg_cur, l[j], u, 0u);
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < kScatterPer; ++j)
-        if (l[j] && !(a.ablate & 4u)) a.lmsg_cur[lp[j]] = mm[j];
-}
-
 __global__ __launch_bounds__(kBlock) void k_gs_link_scatter(RoundArgs a) {
     const uint32_t n = a.g.wired;
     const uint32_t base = blockIdx.x * kBlock * kScatterPer + threadIdx.x;
@@ -419,8 +436,9 @@ __device__ __forceinline__ void put(const Xchg& x, uint32_t q, uint32_t pos, uin
     }
 }
 
-// Sharded k_ps_link_scatter: link messages whose CSR slot belongs to another rank go to that
-// rank's send chunk as (global slot, s, w); the receiver writes them into the same slot.
+// Sharded push-sum link pass: link messages whose CSR slot belongs to another rank go to that
+// rank's send chunk as (global slot, s, w); the receiver writes them into the same slot.  A
+// local receiver gathers the message itself (k_ps_pull<2> reads the link bitmap).
 __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg x) {
     const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
     const uint32_t base = a.lo + blockIdx.x * kBlock * kScatterPer + threadIdx.x;
@@ -442,7 +460,6 @@ __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg 
 #pragma unroll
     for (uint32_t j = 0; j < kScatterPer; ++j) {
         const bool remote = l[j] && (lp[j] < slo || lp[j] >= shi);
-        if (l[j] && !remote) a.lmsg_cur[lp[j]] = mm[j];
         const uint32_t q = remote ? owner(x.sbnd, x.world, lp[j]) : 0u;
         const uint32_t pos = reserve(x, remote, q);
         if (remote) put<true>(x, q, pos, lp[j], mm[j]);
@@ -879,8 +896,9 @@ uint32_t span_for(uint32_t n, int grid) {
 }
 
 void launch_ps_pull(const RoundArgs& a, const Launch& l) {
-    if (a.g.has_link) hipLaunchKernelGGL(k_ps_pull<true>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
-    else hipLaunchKernelGGL(k_ps_pull<false>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+    if (!a.g.has_link) hipLaunchKernelGGL(k_ps_pull<0>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+    else if (!a.sharded) hipLaunchKernelGGL(k_ps_pull<1>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+    else hipLaunchKernelGGL(k_ps_pull<2>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
 }
 
 void launch_gs_pull(const RoundArgs& a, const Launch& l) {
@@ -890,10 +908,6 @@ void launch_gs_pull(const RoundArgs& a, const Launch& l) {
 
 // Flat grids (one actor per thread): a grid-stride loop would make each iteration's load wait
 // behind the previous iteration's scattered store.
-void launch_ps_link_scatter(const RoundArgs& a, const Launch& l) {
-    hipLaunchKernelGGL(k_ps_link_scatter, dim3((a.g.wired + kScatterPer * kBlock - 1) / (kScatterPer * kBlock)), dim3(kBlock), 0, l.stream, a);
-}
-
 void launch_gs_link_scatter(const RoundArgs& a, const Launch& l) {
     hipLaunchKernelGGL(k_gs_link_scatter, dim3((a.g.wired + kScatterPer * kBlock - 1) / (kScatterPer * kBlock)), dim3(kBlock), 0, l.stream, a);
 }

@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libgossip_hip.so")
+# GP_LIB (tuning only): load a variant build, e.g. lib_<name>/ from tools/variants/build.sh
+LIB_PATH = os.path.join(PKG_ROOT, os.environ.get("GP_LIB", "lib"), "libgossip_hip.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "gossip_hip.h")
 
 ABI_VERSION = 2
