@@ -510,6 +510,8 @@ int fill_sums(Handle* h, gp_status* st) {
     return GP_OK;
 }
 
+constexpr int64_t kTimeEvery = 8;
+
 int step(Handle* h, int64_t max_rounds, gp_status* st) {
     if (max_rounds < 0) return fail(GP_EINVAL, "max_rounds < 0");
     if (h->sharded) return fail(GP_ESTATE, "a shard advances with gp_shard_round / gp_shard_deliver");
@@ -524,9 +526,22 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
             if ((rc = launch_round(h, 0, nullptr, false, 0))) return rc;
             h->next_kernel = 1;
         }
-        if (timing && (rc = ensure_events(h, B))) return rc;
-        for (int64_t i = 0; i < B; ++i)
-            if ((rc = launch_round(h, h->next_kernel + i, nullptr, timing, i))) return rc;
+        // Kernel timing.  With no pass after the round kernel, one event pair brackets each group
+        // of kTimeEvery consecutive round kernels (per-launch time = group time / rounds, launch
+        // gaps included); otherwise every kTimeEvery-th round is bracketed kernel by kernel.  Either
+        // way the events stay out of most of the stream (each record costs stream time).
+        const bool group = timing && aux_kernel_name(h)[0] == '\0';
+        const int64_t ng = (B + kTimeEvery - 1) / kTimeEvery;
+        if (timing && (rc = ensure_events(h, ng))) return rc;
+        for (int64_t i = 0; i < B; ++i) {
+            const int64_t j = i / kTimeEvery;
+            if (group && i % kTimeEvery == 0) HIP_TRY(hipEventRecord(h->kev[3 * j], h->stream));
+            if ((rc = launch_round(h, h->next_kernel + i, nullptr, timing && !group && i % kTimeEvery == 0, j))) return rc;
+            if (group && (i % kTimeEvery == kTimeEvery - 1 || i == B - 1)) {
+                HIP_TRY(hipEventRecord(h->kev[3 * j + 1], h->stream));
+                HIP_TRY(hipEventRecord(h->kev[3 * j + 2], h->stream));
+            }
+        }
         h->next_kernel += B;
         // total[] of the last round this batch applied (F(k) applies round k, or k-1 for gossip)
         launch_finalize(h->total, h->parts, h->next_kernel - (h->gossip ? 2 : 1), h->stream);
@@ -551,7 +566,18 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         }
         h->completed = (int64_t)h->h_trace[real - 1];
         h->rounds += real;
-        if (timing && (rc = accumulate_timing(h, real))) return rc;
+        if (group) {  // groups wholly inside the real rounds
+            for (int64_t j = 0; j < ng; ++j) {
+                const int64_t first = j * kTimeEvery, last = std::min<int64_t>(first + kTimeEvery, B) - 1;
+                if (last >= real) break;
+                float ms = 0.f;
+                HIP_TRY(hipEventElapsedTime(&ms, h->kev[3 * j], h->kev[3 * j + 1]));
+                h->k_total_ms += ms;
+                h->k_launches += last - first + 1;
+            }
+        } else if (timing && (rc = accumulate_timing(h, (real + kTimeEvery - 1) / kTimeEvery))) {
+            return rc;
+        }
         h->batch = std::min<int64_t>(h->batch * 2, 256);
     }
     HIP_TRY(hipEventRecord(h->ev_b, h->stream));
