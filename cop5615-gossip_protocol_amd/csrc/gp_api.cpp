@@ -278,15 +278,16 @@ int build_links(Handle* h) {
         h->sbnd[q] = v;
     }
     const int64_t slo = h->sbnd[h->rank], nsl = h->sbnd[h->rank + 1] - slo;
-    if (!h->generic) {  // pull kernels: sender-pushed link slots
-        if (h->gossip) {
-            if ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))) return rc;
-        } else {
+    if (!h->generic) {  // pull kernels
+        // per-slot link counts (gossip; one-GPU push-sum)
+        if ((h->gossip || !h->sharded) &&
+            ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))))
+            return rc;
+        if (!h->gossip && h->sharded) {  // link bitmap of local senders + slots of remote ones
             // one bitmap word per 64 own actors (+1: the last wave may straddle hi)
             const size_t words = ((size_t)h->own() + 63) / 64 + 1;
             if ((rc = h->alloc(&h->lbits[0], words)) || (rc = h->alloc(&h->lbits[1], words))) return rc;
-            if (h->sharded &&
-                ((rc = h->alloc(&h->lmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lmsg[1], (size_t)nsl, slo))))
+            if ((rc = h->alloc(&h->lmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lmsg[1], (size_t)nsl, slo)))
                 return rc;
         }
     }
@@ -400,16 +401,17 @@ const char* round_kernel_name(const Handle* h) {
 const char* aux_kernel_name(const Handle* h) {
     if (h->generic) return h->gossip ? "" : "k_scan_* + k_ps_push_fill";
     if (!h->g.has_link) return "";
-    if (h->gossip) return "k_gs_link_scatter";
-    return h->sharded ? "k_ps_link_scatter_x" : "";  // one GPU: the receiver gathers (no pass)
+    if (h->sharded) return h->gossip ? "k_gs_link_scatter_x" : "k_ps_link_scatter_x";
+    return "k_link_count";
 }
 
 // Compulsory HBM bytes of one launch of the dominant round kernel for its data layout
 // (every array element it must touch, touched once); DESIGN.md §5.
 //   push-sum pull: held (S,W) read 16 + message write 16 + flags read 1 + direction byte read
 //   1 (own row; neighbour rows re-read from cache) + direction write 1 per participant; Imp3D
-//   adds the link CSR offsets (4 per actor), the 4-byte source per link, one bitmap bit per
-//   actor, and the 16-byte message of every link that fired (~1 in 7: the interior degree).
+//   adds the link CSR offsets (4 per actor), per link the 4-byte source and 1-byte slot count,
+//   and the 16-byte message of every link that fired (~1 in 7: the interior degree).  The link
+//   count pass (a separate kernel) is not included.
 //   gossip pull: state byte read 1 + direction byte read 1 + write 1 (+ count r/w 8 on the
 //   receipts, not modelled); Imp3D adds offsets 4 per actor and 1 per link slot.
 double bytes_per_round(const Handle* h) {
@@ -421,7 +423,7 @@ double bytes_per_round(const Handle* h) {
     }
     if (h->generic) return P * (16 + 16 + 16 + 1 + 4 + 4 + 4 + 4 + 4);
     double b = P * (16 + 16 + 1 + 1 + 1);
-    if (h->g.has_link) b += 4 * A + links * 4 + A / 8 + links / 7 * 16;
+    if (h->g.has_link) b += 4 * A + links * (4 + 1) + links / 7 * 16;
     return b;
 }
 
@@ -451,14 +453,15 @@ void launch_aux(Handle* h, int64_t k, const Xchg* x) {
     if (h->gossip) {
         if (!h->generic && h->g.has_link) {
             if (x) launch_gs_link_scatter_x(a, *x, l);
-            else launch_gs_link_scatter(a, l);
+            else launch_link_count(a, l);
         }
     } else if (h->generic) {
         const int c = (int)(r & 1u);
         launch_exclusive_scan(h->bcnt[c], h->boff[c], h->g.actors, h->scan_scratch, h->stream);
         launch_ps_push_fill(a, h->slot[c], h->boff[c], l);
-    } else if (h->g.has_link && x) {
-        launch_ps_link_scatter_x(a, *x, l);
+    } else if (h->g.has_link) {
+        if (x) launch_ps_link_scatter_x(a, *x, l);
+        else launch_link_count(a, l);
     }
 }
 

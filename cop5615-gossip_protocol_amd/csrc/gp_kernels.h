@@ -39,12 +39,10 @@ struct RoundArgs {
     const uint32_t* rev_off;  // CSR of link sources per destination, ascending
     const uint32_t* rev_src;
     const uint32_t* lpos;     // CSR slot of v's own link edge: rev_src[lpos[v]] == v
-    // Gossip: extra-link receipts are PUSHED by the sender into its CSR slot (ping-pong); the
-    // receiver scans its slots in order and empties what it consumed (a u8 chain count set back
-    // to 0).  Sharded push-sum slots hold (s, w), emptied with w = kEmptySlot NaN.
-    // Push-sum (k_ps_pull): the receiver reads a local sender's message from msg_prev after
-    // checking the sender's bit in the link bitmap (bit v - lo; ping-pong); only a sharded
-    // run's remote senders deliver through the CSR slots lmsg (written by the exchange).
+    // Link counts per CSR slot (k_link_count, ping-pong; emptied by the receiver): gossip chains,
+    // or one-GPU push-sum messages that took their link (the receiver then reads msg_prev[u]).
+    // A shard's push-sum instead checks a local sender's bit in the link bitmap (bit u - lo,
+    // ping-pong) and reads a remote sender's message from its CSR slot in lmsg (the exchange).
     uint8_t* lcnt_prev;
     uint8_t* lcnt_cur;
     double2* lmsg_prev;
@@ -119,7 +117,7 @@ uint32_t span_for(uint32_t n, int grid);
 // round kernels
 void launch_ps_pull(const RoundArgs& a, const Launch& l);
 void launch_gs_pull(const RoundArgs& a, const Launch& l);
-void launch_gs_link_scatter(const RoundArgs& a, const Launch& l);
+void launch_link_count(const RoundArgs& a, const Launch& l);
 void launch_ps_push_emit(const RoundArgs& a, const Launch& l);
 void launch_ps_push_fill(const RoundArgs& a, uint32_t* slot_cur, const uint32_t* boff_cur, const Launch& l);
 void launch_gs_push(const RoundArgs& a, const Launch& l);

@@ -232,22 +232,33 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
                 uint32_t ls[kLinkUnroll];
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) ls[k] = load_sel(a.rev_src, k < nl, li + k, a.slot_lo);
-                // ---- level 3: the sources' link bits (a 1.2 MB bitmap at 10M actors: L2-resident);
-                // sharded: a remote source's CSR slot instead (filled by the exchange, emptied here)
+                // ---- level 2 (cont.): one GPU — the per-slot count k_link_count wrote for the
+                // senders whose message took its link (coalesced bytes; emptied here);
+                // ---- level 3, sharded: a local source's link bit, or a remote source's CSR slot
+                // (filled by the exchange, emptied here)
                 bool lk[kLinkUnroll], loc[kLinkUnroll];
                 double2 lm[kLinkUnroll];
+                uint8_t lc[kLinkUnroll];
+                if (LM == 1) {
+#pragma unroll
+                    for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, a.slot_lo);
+                }
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) {
+                    loc[k] = true;
+                    if (LM == 1) {
+                        lk[k] = k < nl && lc[k] != 0;
+                        if (lk[k]) a.lcnt_prev[li + k] = 0;
+                        continue;
+                    }
                     const uint32_t off = ls[k] - a.lo;
-                    loc[k] = LM == 1 || off < a.hi - a.lo;
+                    loc[k] = off < a.hi - a.lo;
                     const unsigned long long w = load_sel(a.lbits_prev, k < nl && loc[k], off >> 6, 0u);
                     lk[k] = k < nl && loc[k] && ((w >> (off & 63u)) & 1ull);
-                    if (LM == 2) {
-                        lm[k] = load_sel(a.lmsg_prev, k < nl && !loc[k], li + k, a.slot_lo);
-                        if (k < nl && !loc[k] && slot_full(lm[k])) {
-                            lk[k] = true;
-                            a.lmsg_prev[li + k].y = __longlong_as_double((long long)kEmptySlot);
-                        }
+                    lm[k] = load_sel(a.lmsg_prev, k < nl && !loc[k], li + k, a.slot_lo);
+                    if (k < nl && !loc[k] && slot_full(lm[k])) {
+                        lk[k] = true;
+                        a.lmsg_prev[li + k].y = __longlong_as_double((long long)kEmptySlot);
                     }
                 }
                 // ---- level 4: the messages of the local sources that took their link to v
@@ -262,7 +273,13 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
                     }
                 for (uint32_t k = kLinkUnroll; k < nl; ++k) {  // rare: more than kLinkUnroll sources
                     const uint32_t u = a.rev_src[li + k];
-                    if (LM == 1 || u - a.lo < a.hi - a.lo) {
+                    if (LM == 1) {
+                        if (a.lcnt_prev[li + k]) {
+                            a.lcnt_prev[li + k] = 0;
+                            flush(u);
+                            add(a.msg_prev[u]);
+                        }
+                    } else if (u - a.lo < a.hi - a.lo) {
                         if (link_bit(a.lbits_prev, u - a.lo)) {
                             flush(u);
                             add(a.msg_prev[u]);
@@ -290,7 +307,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
             ++newly;
         }
         }
-        if (LM) {
+        if (LM == 2) {
             const unsigned long long bits = __ballot(linked);
             if ((threadIdx.x & 63u) == 0u) a.lbits_cur[(v - a.lo) >> 6] = bits;
         }
@@ -366,16 +383,18 @@ __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
     if (r) block_add(newly, a.parts, (long long)r - 1);
 }
 
-// ------------------------------------------------------------------ link scatter passes
-// After F(r): every actor whose round-r message took its extra link (direction code 6) writes
-// it into its CSR slot, where the receiver scans it in F(r+1).  A separate pass so the round
-// kernel's loads never wait behind scattered stores (vmcnt counts stores on CDNA).
-// Four actors per thread (block-strided, so every load instruction stays coalesced): their
-// direction codes, then every link message's slot index and payload in flight together
-// (memory-level parallelism), then the scattered stores.
+// ------------------------------------------------------------------ link count pass
+// After F(r): every actor whose round-r message(s) took its extra link (direction code 6;
+// gossip: per activation chain) writes the count (1 or 2) into its CSR slot lpos[u], a byte
+// the receiver reads — coalesced, in CSR order — in F(r+1) and empties.  Only the ~1/7 of
+// senders that fired touch a random address; the receiver then reads a push-sum message
+// straight from the sender's row (msg_prev[u]).  A separate pass so the round kernel's loads
+// never wait behind scattered stores (vmcnt counts stores on CDNA).  Four actors per thread
+// (block-strided, so every load instruction stays coalesced): their direction codes, then the
+// slot indices in flight together, then the scattered stores.
 constexpr uint32_t kScatterPer = 4;
 
-__global__ __launch_bounds__(kBlock) void k_gs_link_scatter(RoundArgs a) {
+__global__ __launch_bounds__(kBlock) void k_link_count(RoundArgs a) {
     const uint32_t n = a.g.wired;
     const uint32_t base = blockIdx.x * kBlock * kScatterPer + threadIdx.x;
     uint32_t nl[kScatterPer], lp[kScatterPer];
@@ -908,8 +927,8 @@ void launch_gs_pull(const RoundArgs& a, const Launch& l) {
 
 // Flat grids (one actor per thread): a grid-stride loop would make each iteration's load wait
 // behind the previous iteration's scattered store.
-void launch_gs_link_scatter(const RoundArgs& a, const Launch& l) {
-    hipLaunchKernelGGL(k_gs_link_scatter, dim3((a.g.wired + kScatterPer * kBlock - 1) / (kScatterPer * kBlock)), dim3(kBlock), 0, l.stream, a);
+void launch_link_count(const RoundArgs& a, const Launch& l) {
+    hipLaunchKernelGGL(k_link_count, dim3((a.g.wired + kScatterPer * kBlock - 1) / (kScatterPer * kBlock)), dim3(kBlock), 0, l.stream, a);
 }
 
 void launch_ps_push_emit(const RoundArgs& a, const Launch& l) {
