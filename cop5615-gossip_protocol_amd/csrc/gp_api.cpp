@@ -113,7 +113,6 @@ struct Handle {
     uint32_t* lpos = nullptr;
     uint8_t* lcnt[2] = {nullptr, nullptr};   // gossip link slots
     double2* lmsg[2] = {nullptr, nullptr};   // push-sum link slots (sharded: remote senders)
-    unsigned long long* lbits[2] = {nullptr, nullptr};  // push-sum link bitmap, bit v - lo
     // push-sum
     double2* msg[2] = {nullptr, nullptr};
     uint8_t* dir[2] = {nullptr, nullptr};
@@ -210,8 +209,6 @@ struct Handle {
         a.lcnt_cur = lcnt[c];
         a.lmsg_prev = lmsg[p];
         a.lmsg_cur = lmsg[c];
-        a.lbits_prev = lbits[p];
-        a.lbits_cur = lbits[c];
         a.msg_prev = msg[p];
         a.msg_cur = msg[c];
         a.dir_prev = dir[p];
@@ -279,17 +276,12 @@ int build_links(Handle* h) {
     }
     const int64_t slo = h->sbnd[h->rank], nsl = h->sbnd[h->rank + 1] - slo;
     if (!h->generic) {  // pull kernels
-        // per-slot link counts (gossip; one-GPU push-sum)
-        if ((h->gossip || !h->sharded) &&
-            ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))))
+        // per-slot link counts of local senders (gossip chains, push-sum messages)
+        if ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))) return rc;
+        // sharded push-sum: (s, w) of remote senders, written by the exchange
+        if (!h->gossip && h->sharded &&
+            ((rc = h->alloc(&h->lmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lmsg[1], (size_t)nsl, slo))))
             return rc;
-        if (!h->gossip && h->sharded) {  // link bitmap of local senders + slots of remote ones
-            // one bitmap word per 64 own actors (+1: the last wave may straddle hi)
-            const size_t words = ((size_t)h->own() + 63) / 64 + 1;
-            if ((rc = h->alloc(&h->lbits[0], words)) || (rc = h->alloc(&h->lbits[1], words))) return rc;
-            if ((rc = h->alloc(&h->lmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lmsg[1], (size_t)nsl, slo)))
-                return rc;
-        }
     }
     if (h->sharded) {  // link counts per (source rank, destination rank, sender degree)
         const size_t nb = (size_t)h->world * h->world * 8;

@@ -40,15 +40,13 @@ struct RoundArgs {
     const uint32_t* rev_src;
     const uint32_t* lpos;     // CSR slot of v's own link edge: rev_src[lpos[v]] == v
     // Link counts per CSR slot (k_link_count, ping-pong; emptied by the receiver): gossip chains,
-    // or one-GPU push-sum messages that took their link (the receiver then reads msg_prev[u]).
-    // A shard's push-sum instead checks a local sender's bit in the link bitmap (bit u - lo,
-    // ping-pong) and reads a remote sender's message from its CSR slot in lmsg (the exchange).
+    // or push-sum messages that took their link (the receiver then reads msg_prev[u]).  A shard's
+    // push-sum reads a remote sender's (s, w) from its CSR slot in lmsg (written by the exchange;
+    // emptied with w = kEmptySlot).
     uint8_t* lcnt_prev;
     uint8_t* lcnt_cur;
     double2* lmsg_prev;
     double2* lmsg_cur;
-    const unsigned long long* lbits_prev;
-    unsigned long long* lbits_cur;
     // push-sum state
     const double2* msg_prev;  // message emitted in round r-1 (= held S,W when not converged)
     double2* msg_cur;

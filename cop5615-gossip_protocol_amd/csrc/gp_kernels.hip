@@ -147,23 +147,18 @@ __device__ __forceinline__ bool slot_full(double2 m) {
     return (unsigned long long)__double_as_longlong(m.y) != kEmptySlot;
 }
 
-// Link bitmap: bit (v - lo) is set iff actor v's round message took its extra link (direction
-// code 6).  One 64-bit word per wave, written by a ballot: a wave covers 64 consecutive actors
-// starting at a multiple of 64 from lo.
-__device__ __forceinline__ bool link_bit(const unsigned long long* bits, uint32_t off) {
-    return ((bits[off >> 6] >> (off & 63u)) & 1ull) != 0ull;
-}
 // One actor's round (program.fs:119-143 after collecting the round r-1 messages to v).
 // Collect = the canonical sequential fp64 sum, from +0.0, of the messages sent to v in ascending
-// source id.  Messages are never copied: a message IS the sender's held state, so a grid
-// sender's message is read from msg_prev at v-G^2, v-G, v-1, v+1, v+G or v+G^2 (a sender targets
-// v iff its direction byte is the opposite code), and an extra-link sender u (CSR rev_src,
-// ascending) from msg_prev[u] iff u's bit is set in the link bitmap.  Loads are unconditional
-// (clamped addresses) in four dependency levels: (1) own flags, held (S,W), the six neighbours'
-// direction bytes, the CSR range; (2) the first 3 grid hits' messages and the first kLinkUnroll
-// link sources; (3) those sources' bitmap words; (4) the fired links' messages.
-// LM: 0 no extra links; 1 links, every source local; 2 sharded: a source outside [lo, hi)
-// delivers through its CSR slot in lmsg_prev (written by the exchange), emptied after use.
+// source id.  Messages are never copied on one GPU: a message IS the sender's held state, so a
+// grid sender's message is read from msg_prev at v-G^2, v-G, v-1, v+1, v+G or v+G^2 (a sender
+// targets v iff its direction byte is the opposite code), and an extra-link sender u (CSR
+// rev_src, ascending) from msg_prev[u] iff k_link_count marked u's CSR slot.  Loads are
+// unconditional (clamped addresses) in three dependency levels: (1) own flags, held (S,W), the
+// six neighbours' direction bytes, the CSR range; (2) the first 3 grid hits' messages and, per
+// CSR slot of the first kLinkUnroll, the source id and link count (coalesced: CSR order);
+// (3) the messages of the links that fired.
+// LM: 0 no extra links; 1 links; 2 sharded: a source outside [lo, hi) delivers its (s, w)
+// through its CSR slot in lmsg_prev (written by the exchange, emptied here).
 template <int LM>
 __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
     if (gate(a, a.r)) return;
@@ -174,7 +169,6 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
     uint32_t newly = 0;
     for (; v < end; v += step) {
         const uint32_t m = presence(g, v);
-        bool linked = false;
         if (m) {
         const uint32_t code = (a.ablate & 8u) ? kth_bit(m, v % popc(m))
                                               : kth_bit(m, scale_draw(philox_x(v, r, kStreamPush, a.seed), popc(m)));
@@ -232,39 +226,29 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
                 uint32_t ls[kLinkUnroll];
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) ls[k] = load_sel(a.rev_src, k < nl, li + k, a.slot_lo);
-                // ---- level 2 (cont.): one GPU — the per-slot count k_link_count wrote for the
-                // senders whose message took its link (coalesced bytes; emptied here);
-                // ---- level 3, sharded: a local source's link bit, or a remote source's CSR slot
-                // (filled by the exchange, emptied here)
                 bool lk[kLinkUnroll], loc[kLinkUnroll];
                 double2 lm[kLinkUnroll];
                 uint8_t lc[kLinkUnroll];
-                if (LM == 1) {
 #pragma unroll
-                    for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, a.slot_lo);
-                }
+                for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, a.slot_lo);
+                // ---- level 3: the messages of the local sources whose slot k_link_count marked;
+                // sharded: a remote source's CSR slot (filled by the exchange), emptied here
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) {
-                    loc[k] = true;
-                    if (LM == 1) {
-                        lk[k] = k < nl && lc[k] != 0;
-                        if (lk[k]) a.lcnt_prev[li + k] = 0;
-                        continue;
-                    }
-                    const uint32_t off = ls[k] - a.lo;
-                    loc[k] = off < a.hi - a.lo;
-                    const unsigned long long w = load_sel(a.lbits_prev, k < nl && loc[k], off >> 6, 0u);
-                    lk[k] = k < nl && loc[k] && ((w >> (off & 63u)) & 1ull);
-                    lm[k] = load_sel(a.lmsg_prev, k < nl && !loc[k], li + k, a.slot_lo);
-                    if (k < nl && !loc[k] && slot_full(lm[k])) {
-                        lk[k] = true;
-                        a.lmsg_prev[li + k].y = __longlong_as_double((long long)kEmptySlot);
+                    loc[k] = LM == 1 || ls[k] - a.lo < a.hi - a.lo;
+                    lk[k] = k < nl && loc[k] && lc[k] != 0;
+                    if (lk[k]) a.lcnt_prev[li + k] = 0;
+                    lm[k] = load_sel(a.msg_prev, lk[k], ls[k], v);
+                    if (LM == 2) {
+                        const bool rem = k < nl && !loc[k];
+                        const double2 rm = load_sel(a.lmsg_prev, rem, li + k, a.slot_lo);
+                        if (rem && slot_full(rm)) {
+                            lk[k] = true;
+                            lm[k] = rm;
+                            a.lmsg_prev[li + k].y = __longlong_as_double((long long)kEmptySlot);
+                        }
                     }
                 }
-                // ---- level 4: the messages of the local sources that took their link to v
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k)
-                    if (loc[k]) lm[k] = load_sel(a.msg_prev, lk[k], ls[k], v);
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k)
                     if (lk[k]) {
@@ -273,14 +257,9 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
                     }
                 for (uint32_t k = kLinkUnroll; k < nl; ++k) {  // rare: more than kLinkUnroll sources
                     const uint32_t u = a.rev_src[li + k];
-                    if (LM == 1) {
+                    if (LM == 1 || u - a.lo < a.hi - a.lo) {
                         if (a.lcnt_prev[li + k]) {
                             a.lcnt_prev[li + k] = 0;
-                            flush(u);
-                            add(a.msg_prev[u]);
-                        }
-                    } else if (u - a.lo < a.hi - a.lo) {
-                        if (link_bit(a.lbits_prev, u - a.lo)) {
                             flush(u);
                             add(a.msg_prev[u]);
                         }
@@ -300,16 +279,11 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
         const PsOut o = ps_update(f, held, ss, ww, cin, a.delta, a.term_limit);
         if (o.send) a.msg_cur[v] = o.msg;
         a.dir_cur[v] = o.send ? (uint8_t)code : kDirNone;
-        linked = o.send && code == kDirLink;
         if (f != f0) a.flags[v] = f;
         if (o.conv_now) {
             a.frozen[v] = o.msg;
             ++newly;
         }
-        }
-        if (LM == 2) {
-            const unsigned long long bits = __ballot(linked);
-            if ((threadIdx.x & 63u) == 0u) a.lbits_cur[(v - a.lo) >> 6] = bits;
         }
     }
     block_add(newly, a.parts, r);
@@ -455,9 +429,9 @@ __device__ __forceinline__ void put(const Xchg& x, uint32_t q, uint32_t pos, uin
     }
 }
 
-// Sharded push-sum link pass: link messages whose CSR slot belongs to another rank go to that
-// rank's send chunk as (global slot, s, w); the receiver writes them into the same slot.  A
-// local receiver gathers the message itself (k_ps_pull<2> reads the link bitmap).
+// Sharded push-sum link pass: a link message whose CSR slot is this rank's gets the slot's link
+// count (the receiver reads msg_prev[u] itself, as on one GPU); one whose slot belongs to another
+// rank goes to that rank's send chunk as (global slot, s, w), written into the same slot there.
 __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg x) {
     const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
     const uint32_t base = a.lo + blockIdx.x * kBlock * kScatterPer + threadIdx.x;
@@ -479,6 +453,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg 
 #pragma unroll
     for (uint32_t j = 0; j < kScatterPer; ++j) {
         const bool remote = l[j] && (lp[j] < slo || lp[j] >= shi);
+        if (l[j] && !remote) a.lcnt_cur[lp[j]] = 1;
         const uint32_t q = remote ? owner(x.sbnd, x.world, lp[j]) : 0u;
         const uint32_t pos = reserve(x, remote, q);
         if (remote) put<true>(x, q, pos, lp[j], mm[j]);
