@@ -112,7 +112,6 @@ struct Handle {
     uint32_t* rev_src = nullptr;
     uint32_t* lpos = nullptr;
     uint8_t* lcnt[2] = {nullptr, nullptr};   // gossip link slots
-    double2* lmsg[2] = {nullptr, nullptr};   // push-sum link slots (sharded: remote senders)
     // push-sum
     double2* msg[2] = {nullptr, nullptr};
     uint8_t* dir[2] = {nullptr, nullptr};
@@ -147,7 +146,7 @@ struct Handle {
     hipEvent_t ev_a = nullptr, ev_b = nullptr;
     int64_t k_launches = 0;
     double k_total_ms = 0.0, k_aux_ms = 0.0;
-    int64_t timed_first = 0;  // sharded: round index of kev[0..2]
+    std::vector<long long> timed_round;  // sharded: round applied by each timed kernel
     int64_t timed_count = 0;
 
     ~Handle() {
@@ -207,8 +206,6 @@ struct Handle {
         const int c = (int)(r & 1u), p = c ^ 1;
         a.lcnt_prev = lcnt[p];
         a.lcnt_cur = lcnt[c];
-        a.lmsg_prev = lmsg[p];
-        a.lmsg_cur = lmsg[c];
         a.msg_prev = msg[p];
         a.msg_cur = msg[c];
         a.dir_prev = dir[p];
@@ -278,10 +275,7 @@ int build_links(Handle* h) {
     if (!h->generic) {  // pull kernels
         // per-slot link counts of local senders (gossip chains, push-sum messages)
         if ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))) return rc;
-        // sharded push-sum: (s, w) of remote senders, written by the exchange
-        if (!h->gossip && h->sharded &&
-            ((rc = h->alloc(&h->lmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lmsg[1], (size_t)nsl, slo))))
-            return rc;
+
     }
     if (h->sharded) {  // link counts per (source rank, destination rank, sender degree)
         const size_t nb = (size_t)h->world * h->world * 8;
@@ -333,11 +327,10 @@ int reset(Handle* h) {
         HIP_TRY(hipMemsetAsync(h->pcount, 0, (size_t)h->world * sizeof(uint32_t), h->stream));
         HIP_TRY(hipMemsetAsync(h->overflow, 0, sizeof(uint32_t), h->stream));
     }
-    if (h->lcnt[0] || h->lmsg[0]) {  // no link message in flight
+    if (h->lcnt[0]) {  // no link message in flight
         const size_t slo = (size_t)h->sbnd[h->rank], ns = (size_t)(h->sbnd[h->rank + 1] - h->sbnd[h->rank]);
         for (int i = 0; i < 2; ++i) {
             if (h->lcnt[i]) HIP_TRY(hipMemsetAsync(h->lcnt[i] + slo, 0, ns, h->stream));
-            if (h->lmsg[i]) launch_fill_empty_slots(h->lmsg[i] + slo, ns, h->stream);
         }
     }
     if (!h->gossip) {
@@ -387,7 +380,7 @@ int reset(Handle* h) {
 const char* round_kernel_name(const Handle* h) {
     if (h->gossip) return h->generic ? "k_gs_push" : (h->g.has_link ? "k_gs_pull<true>" : "k_gs_pull<false>");
     if (h->generic) return "k_ps_push_emit";
-    return !h->g.has_link ? "k_ps_pull<0>" : (h->sharded ? "k_ps_pull<2>" : "k_ps_pull<1>");
+    return h->g.has_link ? "k_ps_pull<1>" : "k_ps_pull<0>";
 }
 
 const char* aux_kernel_name(const Handle* h) {
@@ -457,6 +450,8 @@ void launch_aux(Handle* h, int64_t k, const Xchg* x) {
     }
 }
 
+constexpr int64_t kTimeEvery = 8;  // kernel timing: one round in 8
+
 int ensure_events(Handle* h, int64_t rounds) {
     const size_t need = (size_t)(3 * rounds);
     if (h->kev.size() >= need) return GP_OK;
@@ -504,8 +499,6 @@ int fill_sums(Handle* h, gp_status* st) {
     }
     return GP_OK;
 }
-
-constexpr int64_t kTimeEvery = 8;
 
 int step(Handle* h, int64_t max_rounds, gp_status* st) {
     if (max_rounds < 0) return fail(GP_EINVAL, "max_rounds < 0");
@@ -727,10 +720,12 @@ int shard_round(Handle* h, void* send) {
     const int64_t k = h->next_kernel;
     int rc;
     if ((rc = ensure_trace(h, k + 4))) return rc;
-    if (timing && (rc = ensure_events(h, h->timed_count + 1))) return rc;
     const Xchg x = make_xchg(h, send, nullptr);
-    if (timing && k >= (h->gossip ? 1 : 0)) {
-        if (h->timed_count == 0) h->timed_first = k;
+    // kernel timing samples every kTimeEvery-th round (event records cost stream time)
+    if (timing && k >= (h->gossip ? 1 : 0) && k % kTimeEvery == 0) {
+        if ((rc = ensure_events(h, h->timed_count + 1))) return rc;
+        h->timed_round.resize((size_t)h->timed_count + 1);
+        h->timed_round[(size_t)h->timed_count] = applied_round(h, k);
         if ((rc = launch_round(h, k, &x, true, h->timed_count))) return rc;
         ++h->timed_count;
     } else if ((rc = launch_round(h, k, &x, false, 0))) {
@@ -802,8 +797,9 @@ int shard_sync(Handle* h, gp_status* st) {
                 break;
             }
         h->completed = (int64_t)t[real - 1];
-        if (h->converged) timed_real = std::max<int64_t>(0, std::min<int64_t>(h->timed_count, h->rounds + real - h->timed_first + (h->gossip ? 1 : 0)));
         h->rounds += real;
+        timed_real = 0;  // sampled kernels that applied a real round (not past convergence)
+        while (timed_real < h->timed_count && h->timed_round[(size_t)timed_real] < h->rounds) ++timed_real;
     }
     int rc;
     if (h->timed_count && (rc = accumulate_timing(h, timed_real))) return rc;
@@ -932,7 +928,12 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
             return bail(rc);
         }
     } else {
-        if ((rc = h->alloc(&h->msg[0], xn, xlo)) || (rc = h->alloc(&h->msg[1], xn, xlo)) ||
+        // a sharded Imp3D run keeps message rows for every actor: a remote extra-link sender's
+        // message is written into its own row by the exchange (k_shard_unpack)
+        const bool global_rows = h->sharded && h->g.has_link;
+        const size_t mn = global_rows ? A : xn;
+        const int64_t mlo = global_rows ? 0 : xlo;
+        if ((rc = h->alloc(&h->msg[0], mn, mlo)) || (rc = h->alloc(&h->msg[1], mn, mlo)) ||
             (rc = h->alloc(&h->flags, n, lo)) || (rc = h->alloc(&h->frozen, n, lo)) ||
             (rc = h->alloc(&h->partials, (size_t)h->grid)))
             return bail(rc);

@@ -9,8 +9,6 @@ constexpr int kMaxGrid = 256 * 16; // 256 CUs x 16 workgroups: grid-stride beyon
 constexpr int kParts = 64;          // completion sub-counters per round (one 64 B line each)
 constexpr int kPartStride = 16;     // u32 words between sub-counters
 constexpr int kPartRing = 4;        // rounds kept in the sub-counter ring
-// empty link slot: w holds this quiet-NaN bit pattern (a real weight is finite and >= 0)
-constexpr unsigned long long kEmptySlot = 0x7FF800000000DEADull;
 constexpr int kMaxWorld = 16;
 
 // One synchronous round kernel F(r) fuses phase 2 of round r-1 (collect the messages sent to
@@ -39,14 +37,11 @@ struct RoundArgs {
     const uint32_t* rev_off;  // CSR of link sources per destination, ascending
     const uint32_t* rev_src;
     const uint32_t* lpos;     // CSR slot of v's own link edge: rev_src[lpos[v]] == v
-    // Link counts per CSR slot (k_link_count, ping-pong; emptied by the receiver): gossip chains,
-    // or push-sum messages that took their link (the receiver then reads msg_prev[u]).  A shard's
-    // push-sum reads a remote sender's (s, w) from its CSR slot in lmsg (written by the exchange;
-    // emptied with w = kEmptySlot).
+    // Link counts per CSR slot (k_link_count or the exchange; ping-pong; emptied by the
+    // receiver): gossip chains, or push-sum messages that took their link (the receiver then
+    // reads msg_prev[u]; a shard's remote sender's row is written by the exchange).
     uint8_t* lcnt_prev;
     uint8_t* lcnt_cur;
-    double2* lmsg_prev;
-    double2* lmsg_cur;
     // push-sum state
     const double2* msg_prev;  // message emitted in round r-1 (= held S,W when not converged)
     double2* msg_cur;
@@ -125,7 +120,7 @@ void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l
 void launch_gs_push_x(const RoundArgs& a, const Xchg& x, const Launch& l);
 // headers of round `applied` (-1: none) into every send chunk; zero the per-peer counters
 void launch_shard_pack(const RoundArgs& a, const Xchg& x, long long applied, hipStream_t s);
-// total[applied] from the headers; link entries into lmsg_cur / lcnt_cur / inc_cur
+// total[applied] from the headers; link entries into msg_cur + lcnt_cur / lcnt_cur / inc_cur
 void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, uint32_t max_cap, int gossip,
                          int full, hipStream_t s);
 // per-(source rank, destination rank, degree) counts of extra links, for the exchange plan
@@ -143,7 +138,6 @@ void launch_lpos(const uint32_t* rev_src, uint32_t nlinks, uint32_t* lpos, const
 size_t scan_scratch_words(uint32_t n);
 void launch_exclusive_scan(const uint32_t* in, uint32_t* off, uint32_t n, uint32_t* scratch, hipStream_t s);
 void launch_fill_u8(uint8_t* p, uint8_t v, size_t n, hipStream_t s);
-void launch_fill_empty_slots(double2* p, size_t n, hipStream_t s);
 // total[a] = total[a-1] + sum of the round-a sub-counters (after the last kernel of a batch)
 void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hipStream_t s);
 void launch_ps_init(uint8_t* flags, const Geom& g, uint32_t lo, uint32_t hi, uint32_t full, uint32_t term_init,

@@ -143,9 +143,6 @@ __device__ __forceinline__ T load_sel(const T* base, bool pred, uint32_t idx, ui
 // Link slots scanned with unrolled loads before the (rare) tail loop.
 constexpr uint32_t kLinkUnroll = 4;
 
-__device__ __forceinline__ bool slot_full(double2 m) {
-    return (unsigned long long)__double_as_longlong(m.y) != kEmptySlot;
-}
 
 // One actor's round (program.fs:119-143 after collecting the round r-1 messages to v).
 // Collect = the canonical sequential fp64 sum, from +0.0, of the messages sent to v in ascending
@@ -157,8 +154,8 @@ __device__ __forceinline__ bool slot_full(double2 m) {
 // six neighbours' direction bytes, the CSR range; (2) the first 3 grid hits' messages and, per
 // CSR slot of the first kLinkUnroll, the source id and link count (coalesced: CSR order);
 // (3) the messages of the links that fired.
-// LM: 0 no extra links; 1 links; 2 sharded: a source outside [lo, hi) delivers its (s, w)
-// through its CSR slot in lmsg_prev (written by the exchange, emptied here).
+// LM: 0 no extra links; 1 links.  A shard's remote link senders are no different: the exchange
+// writes their (s, w) into their own (global) rows of msg and marks their CSR slots.
 template <int LM>
 __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
     if (gate(a, a.r)) return;
@@ -226,28 +223,17 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
                 uint32_t ls[kLinkUnroll];
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) ls[k] = load_sel(a.rev_src, k < nl, li + k, a.slot_lo);
-                bool lk[kLinkUnroll], loc[kLinkUnroll];
+                bool lk[kLinkUnroll];
                 double2 lm[kLinkUnroll];
                 uint8_t lc[kLinkUnroll];
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, a.slot_lo);
-                // ---- level 3: the messages of the local sources whose slot k_link_count marked;
-                // sharded: a remote source's CSR slot (filled by the exchange), emptied here
+                // ---- level 3: the messages of the sources whose slot is marked
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) {
-                    loc[k] = LM == 1 || ls[k] - a.lo < a.hi - a.lo;
-                    lk[k] = k < nl && loc[k] && lc[k] != 0;
+                    lk[k] = k < nl && lc[k] != 0;
                     if (lk[k]) a.lcnt_prev[li + k] = 0;
                     lm[k] = load_sel(a.msg_prev, lk[k], ls[k], v);
-                    if (LM == 2) {
-                        const bool rem = k < nl && !loc[k];
-                        const double2 rm = load_sel(a.lmsg_prev, rem, li + k, a.slot_lo);
-                        if (rem && slot_full(rm)) {
-                            lk[k] = true;
-                            lm[k] = rm;
-                            a.lmsg_prev[li + k].y = __longlong_as_double((long long)kEmptySlot);
-                        }
-                    }
                 }
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k)
@@ -256,20 +242,11 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
                         add(lm[k]);
                     }
                 for (uint32_t k = kLinkUnroll; k < nl; ++k) {  // rare: more than kLinkUnroll sources
-                    const uint32_t u = a.rev_src[li + k];
-                    if (LM == 1 || u - a.lo < a.hi - a.lo) {
-                        if (a.lcnt_prev[li + k]) {
-                            a.lcnt_prev[li + k] = 0;
-                            flush(u);
-                            add(a.msg_prev[u]);
-                        }
-                    } else {
-                        const double2 mm = a.lmsg_prev[li + k];
-                        if (slot_full(mm)) {
-                            flush(u);
-                            add(mm);
-                            a.lmsg_prev[li + k].y = __longlong_as_double((long long)kEmptySlot);
-                        }
+                    if (a.lcnt_prev[li + k]) {
+                        const uint32_t u = a.rev_src[li + k];
+                        a.lcnt_prev[li + k] = 0;
+                        flush(u);
+                        add(a.msg_prev[u]);
                     }
                 }
             }
@@ -534,7 +511,10 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
             }
             if (full) atomicAdd(&a.inc_cur[t], 1u);
             else if (gossip) a.lcnt_cur[t] = (uint8_t)((e >> 31) + 1u);
-            else a.lmsg_cur[t] = in.msg[i];
+            else {  // the sender's message into its own row; its slot marked for the receiver
+                a.msg_cur[a.rev_src[t]] = in.msg[i];
+                a.lcnt_cur[t] = 1;
+            }
         }
     }
 }
@@ -820,10 +800,6 @@ __global__ void k_fill_u8(uint8_t* p, uint8_t val, size_t n) {
         p[i] = val;
 }
 
-__global__ void k_fill_empty(double2* p, size_t n) {
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        p[i] = make_double2(0.0, __longlong_as_double((long long)kEmptySlot));
-}
 
 __global__ void k_finalize(unsigned long long* total, uint32_t* parts, long long a) {
     unsigned long long x = *part_slot(parts, a, threadIdx.x);
@@ -891,8 +867,7 @@ uint32_t span_for(uint32_t n, int grid) {
 
 void launch_ps_pull(const RoundArgs& a, const Launch& l) {
     if (!a.g.has_link) hipLaunchKernelGGL(k_ps_pull<0>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
-    else if (!a.sharded) hipLaunchKernelGGL(k_ps_pull<1>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
-    else hipLaunchKernelGGL(k_ps_pull<2>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+    else hipLaunchKernelGGL(k_ps_pull<1>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
 }
 
 void launch_gs_pull(const RoundArgs& a, const Launch& l) {
@@ -989,12 +964,6 @@ void launch_fill_u8(uint8_t* p, uint8_t v, size_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_fill_u8, dim3((unsigned)blocks), dim3(kBlock), 0, s, p, v, n);
 }
 
-void launch_fill_empty_slots(double2* p, size_t n, hipStream_t s) {
-    size_t blocks = (n + kBlock - 1) / kBlock;
-    if (blocks > (size_t)kMaxGrid) blocks = kMaxGrid;
-    if (blocks == 0) return;
-    hipLaunchKernelGGL(k_fill_empty, dim3((unsigned)blocks), dim3(kBlock), 0, s, p, n);
-}
 
 void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, total, parts, a);
