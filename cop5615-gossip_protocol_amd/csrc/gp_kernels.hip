@@ -346,6 +346,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
 constexpr uint32_t kScatterPer = 4;
 
 __global__ __launch_bounds__(kBlock) void k_link_count(RoundArgs a) {
+    if (a.r >= 1 && a.total[a.r - 1] >= a.target) return;  // past convergence (F(r) published it)
     const uint32_t n = a.g.wired;
     const uint32_t base = blockIdx.x * kBlock * kScatterPer + threadIdx.x;
     uint32_t nl[kScatterPer], lp[kScatterPer];
