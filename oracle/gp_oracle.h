@@ -81,6 +81,22 @@ int  gpo_shard_round(void* h, void* send);
 int  gpo_shard_deliver(void* h, const void* recv);
 int  gpo_shard_sync(void* h, gpo_status* st);
 
+/* Asynchronous actor run (gp_async.c): the reference's Akka execution model — per-actor FIFO
+ * mailboxes, a seeded random interleaving of runnable actors — over the same neighbour lists
+ * and leader, for statistical sanity checks only.  Time unit: one processed
+ * message.  Any output pointer may be NULL; arrays hold `actors` entries. */
+typedef struct {
+    int64_t steps;      /* messages processed                                   */
+    int64_t completed;  /* reports received by the parent                      */
+    int32_t converged;  /* completed >= nodes                                   */
+    int32_t pad;
+    int64_t messages;   /* messages sent (incl. kick-off and self-activations)  */
+    double sum_s, sum_w; /* push-sum mass held + in mailboxes                   */
+} gpo_async_status;
+
+int gpo_async_run(const gpo_config* cfg, int64_t max_steps, gpo_async_status* st, uint32_t* cnt, double* S,
+                  double* W, uint8_t* flags);
+
 #ifdef __cplusplus
 }
 #endif

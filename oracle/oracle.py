@@ -33,6 +33,11 @@ class Status(C.Structure):
                 ("pad", C.c_int32), ("sum_s", C.c_double), ("sum_w", C.c_double)]
 
 
+class AsyncStatus(C.Structure):
+    _fields_ = [("steps", C.c_int64), ("completed", C.c_int64), ("converged", C.c_int32), ("pad", C.c_int32),
+                ("messages", C.c_int64), ("sum_s", C.c_double), ("sum_w", C.c_double)]
+
+
 _lib = None
 
 
@@ -67,6 +72,7 @@ def lib():
         L.gpo_shard_round.argtypes = [P, P]
         L.gpo_shard_deliver.argtypes = [P, P]
         L.gpo_shard_sync.argtypes = [P, C.POINTER(Status)]
+        L.gpo_async_run.argtypes = [C.POINTER(Config), C.c_int64, C.POINTER(AsyncStatus), P, P, P, P]
         _lib = L
     return _lib
 
@@ -225,3 +231,23 @@ class OracleShard(OracleSim):
 
     def read_messages(self):
         return self._own(super().read_messages())
+
+
+def async_run(n_arg, topology, algo, seed=1, max_steps=50_000_000, delta=1e-10, gossip_threshold=10,
+              term_init=1, term_limit=3):
+    """The reference's asynchronous actor execution (gp_async.c) on the same neighbour lists and
+    leader: a statistical sanity check of the round engine, not a parity oracle.  Returns
+    (status, per-actor arrays {cnt, S, W, flags})."""
+    t = TOPOLOGIES[topology] if isinstance(topology, str) else topology
+    a = ALGOS[algo] if isinstance(algo, str) else algo
+    cfg = Config(n_arg, t, a, seed, delta, gossip_threshold, term_init, term_limit)
+    _, actors, _ = sizes(n_arg, t)
+    cnt = np.zeros(actors, np.uint32)
+    S = np.zeros(actors, np.float64)
+    W = np.zeros(actors, np.float64)
+    flags = np.zeros(actors, np.uint8)
+    st = AsyncStatus()
+    rc = lib().gpo_async_run(C.byref(cfg), max_steps, C.byref(st), _ptr(cnt), _ptr(S), _ptr(W), _ptr(flags))
+    if rc:
+        raise RuntimeError(f"gpo_async_run failed ({rc})")
+    return st, {"cnt": cnt, "S": S, "W": W, "flags": flags}
