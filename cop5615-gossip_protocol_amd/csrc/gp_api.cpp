@@ -71,8 +71,9 @@ int sizes(int64_t n_arg, int32_t topology, int64_t* nodes, int64_t* actors, int6
 
 // Layout of one exchange chunk (peer p -> peer q); both ends compute it identically.
 struct Chunk {
-    size_t hdir = 0, hmsg = 0, slot = 0, msg = 0, size = 0;  // byte offsets / total size
+    size_t hdir = 0, hslot = 0, hmsg = 0, slot = 0, msg = 0, size = 0;  // byte offsets / total size
     uint32_t halo = 0;  // halo actors carried (0: none)
+    uint32_t hcap = 0;  // halo entries: push-sum messages crossing the face
     uint32_t cap = 0;   // link / receipt entries
 };
 
@@ -324,7 +325,7 @@ int reset(Handle* h) {
     HIP_TRY(hipMemsetAsync(h->total, 0, (size_t)h->total_cap * sizeof(unsigned long long), h->stream));
     HIP_TRY(hipMemsetAsync(h->parts, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t), h->stream));
     if (h->sharded) {
-        HIP_TRY(hipMemsetAsync(h->pcount, 0, (size_t)h->world * sizeof(uint32_t), h->stream));
+        HIP_TRY(hipMemsetAsync(h->pcount, 0, ((size_t)h->world + 2) * sizeof(uint32_t), h->stream));
         HIP_TRY(hipMemsetAsync(h->overflow, 0, sizeof(uint32_t), h->stream));
     }
     if (h->lcnt[0]) {  // no link message in flight
@@ -618,8 +619,18 @@ Chunk chunk_layout(const Handle* h, int p, int q) {
         c.hdir = off;
         off = align_up(off + c.halo);
         if (!h->gossip) {
+            // each face actor crosses with probability 1/degree (one uniform draw per round)
+            const int64_t first = q < p ? h->abnd[p] : h->abnd[p + 1] - c.halo;
+            double mean = 0.0;
+            for (int64_t u = first; u < first + c.halo; ++u) {
+                const uint32_t m = presence(h->g, (uint32_t)u);
+                if (m) mean += 1.0 / (double)__builtin_popcount(m);
+            }
+            c.hcap = std::max<uint32_t>(1u, entry_cap(mean, (double)c.halo));
+            c.hslot = off;
+            off = align_up(off + (size_t)c.hcap * sizeof(uint32_t));
             c.hmsg = off;
-            off = align_up(off + (size_t)c.halo * sizeof(double2));
+            off = align_up(off + (size_t)c.hcap * sizeof(double2));
         }
     }
     double mean = 0.0, exact = 0.0;
@@ -669,7 +680,7 @@ int build_plan(Handle* h) {
     h->send_total = so;
     h->recv_total = ro;
     int rc;
-    if ((rc = h->alloc(&h->pcount, (size_t)W)) || (rc = h->alloc(&h->overflow, 1)) || (rc = h->alloc(&h->self_newly, 1)))
+    if ((rc = h->alloc(&h->pcount, (size_t)W + 2)) || (rc = h->alloc(&h->overflow, 1)) || (rc = h->alloc(&h->self_newly, 1)))
         return rc;
     return GP_OK;
 }
@@ -706,6 +717,38 @@ Xchg make_xchg(const Handle* h, void* send, const void* recv) {
                              c.msg ? reinterpret_cast<const double2*>(b + c.msg) : nullptr, c.cap};
         }
     }
+    // halo faces (side 0: rank-1, side 1: rank+1); the crossing code is -x/+x on a line, -z/+z on a grid
+    const int p = h->rank;
+    for (int side = 0; side < 2; ++side) {
+        const int q = side ? p + 1 : p - 1;
+        if (q < 0 || q >= h->world) continue;
+        x.h.code[side] = h->g.gz > 1 ? (side ? 5u : 4u) : (side ? 1u : 0u);
+        const Chunk& co = h->out_chunk[q];
+        if (send && co.halo) {
+            char* b = static_cast<char*>(send) + h->out_off[q];
+            x.h.out_n[side] = co.halo;
+            x.h.out_first[side] = side ? h->hi - co.halo : h->lo;
+            x.h.out_cap[side] = co.hcap;
+            x.h.out_dir[side] = reinterpret_cast<uint8_t*>(b + co.hdir);
+            if (co.hcap) {
+                x.h.out_slot[side] = reinterpret_cast<uint32_t*>(b + co.hslot);
+                x.h.out_msg[side] = reinterpret_cast<double2*>(b + co.hmsg);
+            }
+        }
+        const Chunk& ci = h->in_chunk[q];
+        if (recv && ci.halo) {
+            const char* b = static_cast<const char*>(recv) + h->in_off[q];
+            x.h.in_n[side] = ci.halo;
+            x.h.in_first[side] = side ? h->hi : h->lo - ci.halo;
+            x.h.in_cap[side] = ci.hcap;
+            x.h.in_hdr[side] = reinterpret_cast<const ShardHeader*>(b);
+            x.h.in_dir[side] = reinterpret_cast<const uint8_t*>(b + ci.hdir);
+            if (ci.hcap) {
+                x.h.in_slot[side] = reinterpret_cast<const uint32_t*>(b + ci.hslot);
+                x.h.in_msg[side] = reinterpret_cast<const double2*>(b + ci.hmsg);
+            }
+        }
+    }
     return x;
 }
 
@@ -732,19 +775,9 @@ int shard_round(Handle* h, void* send) {
         return rc;
     }
     const RoundArgs a = h->args((uint32_t)k);
+    // halo faces (this rank's first actors to rank-1, its last actors to rank+1), then the headers
+    launch_shard_halo(a, x, h->gossip ? 0 : 1, h->stream);
     launch_shard_pack(a, x, applied_round(h, k), h->stream);
-    // halo faces: this rank's first actors to rank-1, its last actors to rank+1
-    const int p = h->rank;
-    for (int q : {p - 1, p + 1}) {
-        if (q < 0 || q >= h->world || !h->out_chunk[q].halo) continue;
-        const Chunk& c = h->out_chunk[q];
-        const uint32_t first = q < p ? h->lo : h->hi - c.halo;
-        char* b = static_cast<char*>(send) + h->out_off[q];
-        HIP_TRY(hipMemcpyAsync(b + c.hdir, h->dir[k & 1] + first, c.halo, hipMemcpyDeviceToDevice, h->stream));
-        if (!h->gossip)
-            HIP_TRY(hipMemcpyAsync(b + c.hmsg, h->msg[k & 1] + first, (size_t)c.halo * sizeof(double2),
-                                   hipMemcpyDeviceToDevice, h->stream));
-    }
     HIP_TRY(hipGetLastError());
     h->awaiting_deliver = true;
     h->pending_send = send;
@@ -756,20 +789,11 @@ int shard_deliver(Handle* h, const void* recv) {
     if (!recv && h->recv_total) return fail(GP_EINVAL, "null receive buffer");
     if (reinterpret_cast<uintptr_t>(recv) % kAlign) return fail(GP_EINVAL, "receive buffer not %zu-byte aligned", kAlign);
     const int64_t k = h->next_kernel;
-    const int p = h->rank;
-    for (int q : {p - 1, p + 1}) {  // rank-1's last actors sit below lo, rank+1's first at hi
-        if (q < 0 || q >= h->world || !h->in_chunk[q].halo) continue;
-        const Chunk& c = h->in_chunk[q];
-        const uint32_t first = q < p ? h->lo - c.halo : h->hi;
-        const char* b = static_cast<const char*>(recv) + h->in_off[q];
-        HIP_TRY(hipMemcpyAsync(h->dir[k & 1] + first, b + c.hdir, c.halo, hipMemcpyDeviceToDevice, h->stream));
-        if (!h->gossip)
-            HIP_TRY(hipMemcpyAsync(h->msg[k & 1] + first, b + c.hmsg, (size_t)c.halo * sizeof(double2),
-                                   hipMemcpyDeviceToDevice, h->stream));
-    }
+    // the halo faces (rank-1's last actors land below lo, rank+1's first at hi) and the link
+    // entries are applied by one kernel
     const Xchg x = make_xchg(h, h->pending_send, recv);
-    launch_shard_unpack(h->args((uint32_t)k), x, applied_round(h, k), h->max_in_cap, h->gossip ? 1 : 0,
-                        h->full ? 1 : 0, h->stream);
+    launch_shard_unpack(h->args((uint32_t)k), x, applied_round(h, k), std::max(h->max_in_cap, h->halo),
+                        h->gossip ? 1 : 0, h->full ? 1 : 0, h->stream);
     HIP_TRY(hipGetLastError());
     h->awaiting_deliver = false;
     h->next_kernel = k + 1;

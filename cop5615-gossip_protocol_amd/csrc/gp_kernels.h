@@ -64,14 +64,17 @@ struct RoundArgs {
 };
 
 // Shard exchange (gp_shard_*).  Send chunk to peer q (built by this rank) and receive chunk from
-// peer q (built by q for this rank) share one layout: a 256-byte header, the halo face (direction
-// bytes, then push-sum messages) when q is a z-neighbour, then `cap` link entries: u32 slot (global
-// link-CSR slot; gossip: slot | (chains-1) << 31; full gossip: the target actor), then push-sum
-// (s, w) pairs.  See DESIGN.md §6.
+// peer q (built by q for this rank) share one layout: a 256-byte header; when q is a z-neighbour
+// (rank +-1) the halo face: the direction bytes of the face plane, then (push-sum) `hcap` halo
+// entries, u32 face offsets then (s, w) pairs, for the messages that cross the face only; then
+// `cap` link entries: u32 slot (global link-CSR slot; gossip: slot | (chains-1) << 31; full
+// gossip: the target actor), then push-sum (s, w) pairs.  See DESIGN.md §6.
 struct ShardHeader {
     unsigned long long newly;  // actors that reported in the round (sender's range)
     uint32_t nlinks;           // link entries written (<= cap)
     uint32_t overflow;         // sender dropped entries: the run is void (GP_EOVERFLOW)
+    uint32_t nhalo;            // halo entries written (<= hcap)
+    uint32_t pad;
 };
 
 struct PeerOut {
@@ -88,15 +91,32 @@ struct PeerIn {
     uint32_t cap;
 };
 
+// The halo faces of a shard, side 0 = rank-1 (this rank's first plane / the halo below lo),
+// side 1 = rank+1 (last plane / the halo from hi).  n == 0: no such neighbour.
+struct HaloX {
+    uint32_t out_first[2], out_n[2], out_cap[2];  // face actors sent (global ids), entry capacity
+    uint32_t in_first[2], in_n[2], in_cap[2];     // halo rows received
+    uint32_t code[2];                             // direction code that crosses the face
+    uint8_t* out_dir[2];
+    uint32_t* out_slot[2];
+    double2* out_msg[2];
+    const ShardHeader* in_hdr[2];
+    const uint8_t* in_dir[2];
+    const uint32_t* in_slot[2];
+    const double2* in_msg[2];
+};
+
 struct Xchg {
     uint32_t world, rank;
     uint32_t abnd[kMaxWorld + 1];  // actor range of every rank
     uint32_t sbnd[kMaxWorld + 1];  // link-slot range of every rank (global CSR numbering)
-    uint32_t* pcount;              // per-peer entry counters of the current round (zeroed by pack)
+    uint32_t* pcount;              // per-peer entry counters of the current round, then the two halo
+                                   // entry counters (zeroed by pack)
     uint32_t* overflow;            // sticky local overflow flag
     unsigned long long* self_newly;  // this rank's count of the round (pack -> unpack)
     PeerOut out[kMaxWorld];
     PeerIn in[kMaxWorld];
+    HaloX h;
 };
 
 struct Launch {
@@ -118,9 +138,12 @@ void launch_gs_push(const RoundArgs& a, const Launch& l);
 void launch_ps_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);
 void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);
 void launch_gs_push_x(const RoundArgs& a, const Xchg& x, const Launch& l);
+// halo faces of F(k) into the send chunks of rank +-1: direction bytes, crossing push-sum messages
+void launch_shard_halo(const RoundArgs& a, const Xchg& x, int pushsum, hipStream_t s);
 // headers of round `applied` (-1: none) into every send chunk; zero the per-peer counters
 void launch_shard_pack(const RoundArgs& a, const Xchg& x, long long applied, hipStream_t s);
-// total[applied] from the headers; link entries into msg_cur + lcnt_cur / lcnt_cur / inc_cur
+// total[applied] from the headers; halo faces into the halo rows of dir_cur / msg_cur; link
+// entries into msg_cur + lcnt_cur / lcnt_cur / inc_cur
 void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, uint32_t max_cap, int gossip,
                          int full, hipStream_t s);
 // per-(source rank, destination rank, degree) counts of extra links, for the exchange plan

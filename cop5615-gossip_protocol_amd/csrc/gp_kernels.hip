@@ -421,16 +421,20 @@ __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg 
         l[j] = u < n && load_sel(a.dir_cur, u < n, u, a.lo) == kDirLink;
     }
     uint32_t lp[kScatterPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j) lp[j] = load_sel(a.lpos, l[j], base + j * kBlock, a.lo);
+    // only a remote link needs its message: the fired ~1/7 of senders would otherwise pull in
+    // ~70% of msg_cur's lines (8 messages per 128 B line)
+    bool rm[kScatterPer];
     double2 mm[kScatterPer];
 #pragma unroll
     for (uint32_t j = 0; j < kScatterPer; ++j) {
-        const uint32_t u = base + j * kBlock;
-        lp[j] = load_sel(a.lpos, l[j], u, a.lo);
-        mm[j] = load_sel(a.msg_cur, l[j], u, a.lo);
+        rm[j] = l[j] && (lp[j] < slo || lp[j] >= shi);
+        mm[j] = load_sel(a.msg_cur, rm[j], base + j * kBlock, a.lo);
     }
 #pragma unroll
     for (uint32_t j = 0; j < kScatterPer; ++j) {
-        const bool remote = l[j] && (lp[j] < slo || lp[j] >= shi);
+        const bool remote = rm[j];
         if (l[j] && !remote) a.lcnt_cur[lp[j]] = 1;
         const uint32_t q = remote ? owner(x.sbnd, x.world, lp[j]) : 0u;
         const uint32_t pos = reserve(x, remote, q);
@@ -461,6 +465,51 @@ __global__ __launch_bounds__(kBlock) void k_gs_link_scatter_x(RoundArgs a, Xchg 
     }
 }
 
+// Halo faces of F(k), after the round kernel: the direction bytes of this rank's first plane go
+// to rank-1 and of its last plane to rank+1 (coalesced copies), and of the push-sum messages only
+// those that cross the face (about 1/7 of the plane) as (face offset, s, w) entries.  The
+// receiver's halo rows keep stale messages elsewhere; its pull kernel reads a halo message only
+// when the direction byte points across, so they are never read.
+__device__ __forceinline__ uint32_t reserve1(uint32_t* ctr, bool want) {
+    const unsigned long long mask = __ballot(want);
+    if (!mask) return 0u;
+    const int leader = __ffsll((long long)mask) - 1;
+    uint32_t base = 0;
+    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(ctr, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader, 64);
+    return base + lanes_below(mask);
+}
+
+__global__ __launch_bounds__(kBlock) void k_shard_halo(RoundArgs a, Xchg x, int pushsum) {
+    for (int side = 0; side < 2; ++side) {
+        const uint32_t n = x.h.out_n[side];
+        const uint32_t first = x.h.out_first[side], code = x.h.code[side], cap = x.h.out_cap[side];
+        uint8_t* odir = x.h.out_dir[side];
+        uint32_t* oslot = x.h.out_slot[side];
+        double2* omsg = x.h.out_msg[side];
+        uint32_t* ctr = x.pcount + x.world + side;
+        // block-uniform trip count: every lane of a wave reaches reserve1
+        for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+            const uint32_t i = base + threadIdx.x;
+            const bool valid = i < n;
+            const uint8_t b = load_sel(a.dir_cur, valid, first + i, first);
+            if (valid) odir[i] = b;
+            const bool cross = pushsum && valid && b == code;
+            double2 m = make_double2(0.0, 0.0);
+            if (pushsum) m = load_sel(a.msg_cur, cross, first + i, first);  // gossip: no msg array
+            const uint32_t pos = reserve1(ctr, cross);
+            if (cross) {
+                if (pos < cap) {
+                    oslot[pos] = i;
+                    omsg[pos] = m;
+                } else {
+                    atomicOr(x.overflow, 1u);
+                }
+            }
+        }
+    }
+}
+
 // Round `applied`'s count into every send header; the per-peer counters restart at 0.
 __global__ void k_shard_pack(RoundArgs a, Xchg x, long long applied) {
     unsigned long long newly = 0;
@@ -475,6 +524,16 @@ __global__ void k_shard_pack(RoundArgs a, Xchg x, long long applied) {
         h.newly = newly;
         h.nlinks = c < x.out[q].cap ? c : x.out[q].cap;
         h.overflow = (c > x.out[q].cap || *x.overflow) ? 1u : 0u;
+        h.nhalo = 0u;
+        h.pad = 0u;
+        const int side = q + 1 == x.rank ? 0 : q == x.rank + 1 ? 1 : -1;
+        if (side >= 0) {
+            uint32_t* hc = x.pcount + x.world + side;
+            const uint32_t n = *hc;
+            h.nhalo = n < x.h.out_cap[side] ? n : x.h.out_cap[side];
+            if (n > x.h.out_cap[side]) h.overflow = 1u;
+            *hc = 0u;
+        }
         *x.out[q].hdr = h;
         x.pcount[q] = 0u;
     }
@@ -494,6 +553,25 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
             }
         a.total[applied] = (applied >= 1 ? a.total[applied - 1] : 0ull) + t;
         if (of) atomicOr(x.overflow, 1u);
+    }
+    // halo faces: direction bytes of the neighbour's face plane, then its crossing messages
+    const uint32_t gtid = blockIdx.x * kBlock + threadIdx.x, gstride = gridDim.x * kBlock;
+    for (int side = 0; side < 2; ++side) {
+        const uint32_t n = x.h.in_n[side], first = x.h.in_first[side];
+        if (!n) continue;
+        const uint8_t* idir = x.h.in_dir[side];
+        for (uint32_t i = gtid; i < n; i += gstride) a.dir_cur[first + i] = idir[i];
+        if (!x.h.in_slot[side]) continue;
+        uint32_t ne = x.h.in_hdr[side]->nhalo;
+        ne = ne < x.h.in_cap[side] ? ne : x.h.in_cap[side];
+        for (uint32_t i = gtid; i < ne; i += gstride) {
+            const uint32_t o = x.h.in_slot[side][i];
+            if (o >= n) {
+                atomicOr(x.overflow, 2u);
+                continue;
+            }
+            a.msg_cur[first + o] = x.h.in_msg[side][i];
+        }
     }
     // an entry outside this rank's actors / slots can only come from a corrupt chunk: it is
     // reported (GP_EOVERFLOW at the next sync), never written
@@ -909,6 +987,14 @@ void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l
 
 void launch_gs_push_x(const RoundArgs& a, const Xchg& x, const Launch& l) {
     hipLaunchKernelGGL(k_gs_push_x, dim3(l.grid), dim3(kBlock), 0, l.stream, a, x);
+}
+
+void launch_shard_halo(const RoundArgs& a, const Xchg& x, int pushsum, hipStream_t s) {
+    const uint32_t n = x.h.out_n[0] > x.h.out_n[1] ? x.h.out_n[0] : x.h.out_n[1];
+    if (!n) return;
+    uint32_t blocks = (n + kBlock - 1) / kBlock;
+    blocks = blocks > (uint32_t)kMaxGrid ? (uint32_t)kMaxGrid : blocks;
+    hipLaunchKernelGGL(k_shard_halo, dim3(blocks), dim3(kBlock), 0, s, a, x, pushsum);
 }
 
 void launch_shard_pack(const RoundArgs& a, const Xchg& x, long long applied, hipStream_t s) {
