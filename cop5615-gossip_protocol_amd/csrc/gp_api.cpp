@@ -113,6 +113,7 @@ struct Handle {
     uint32_t* rev_src = nullptr;
     uint32_t* lpos = nullptr;
     uint8_t* lcnt[2] = {nullptr, nullptr};   // gossip link slots
+    double2* rmsg[2] = {nullptr, nullptr};   // shards, push-sum: remote senders' link messages per CSR slot
     // push-sum
     double2* msg[2] = {nullptr, nullptr};
     uint8_t* dir[2] = {nullptr, nullptr};
@@ -209,6 +210,8 @@ struct Handle {
         a.lcnt_cur = lcnt[c];
         a.msg_prev = msg[p];
         a.msg_cur = msg[c];
+        a.rmsg_prev = rmsg[p];
+        a.rmsg_cur = rmsg[c];
         a.dir_prev = dir[p];
         a.dir_cur = dir[c];
         a.flags = flags;
@@ -276,6 +279,10 @@ int build_links(Handle* h) {
     if (!h->generic) {  // pull kernels
         // per-slot link counts of local senders (gossip chains, push-sum messages)
         if ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))) return rc;
+        // a remote sender's link message lands in the receiver's slot, read in CSR order (k_ps_pull<2>)
+        if (h->sharded && h->world > 1 && !h->gossip &&
+            ((rc = h->alloc(&h->rmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->rmsg[1], (size_t)nsl, slo))))
+            return rc;
 
     }
     if (h->sharded) {  // link counts per (source rank, destination rank, sender degree)
@@ -325,7 +332,7 @@ int reset(Handle* h) {
     HIP_TRY(hipMemsetAsync(h->total, 0, (size_t)h->total_cap * sizeof(unsigned long long), h->stream));
     HIP_TRY(hipMemsetAsync(h->parts, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t), h->stream));
     if (h->sharded) {
-        HIP_TRY(hipMemsetAsync(h->pcount, 0, ((size_t)h->world + 2) * sizeof(uint32_t), h->stream));
+        HIP_TRY(hipMemsetAsync(h->pcount, 0, ((size_t)h->world + 2) * kSub * kCtrStride * sizeof(uint32_t), h->stream));
         HIP_TRY(hipMemsetAsync(h->overflow, 0, sizeof(uint32_t), h->stream));
     }
     if (h->lcnt[0]) {  // no link message in flight
@@ -381,7 +388,7 @@ int reset(Handle* h) {
 const char* round_kernel_name(const Handle* h) {
     if (h->gossip) return h->generic ? "k_gs_push" : (h->g.has_link ? "k_gs_pull<true>" : "k_gs_pull<false>");
     if (h->generic) return "k_ps_push_emit";
-    return h->g.has_link ? "k_ps_pull<1>" : "k_ps_pull<0>";
+    return h->g.has_link ? (h->rmsg[0] ? "k_ps_pull<2>" : "k_ps_pull<1>") : "k_ps_pull<0>";
 }
 
 const char* aux_kernel_name(const Handle* h) {
@@ -603,11 +610,15 @@ int partition(int64_t n_arg, int32_t topology, int32_t world, std::vector<int64_
     return GP_OK;
 }
 
-// Entries per round from rank p to rank q, bounded: the exact maximum when small, otherwise the
-// mean + 8 sigma of its (binomial) distribution — an overflow is reported, never dropped.
-uint32_t entry_cap(double mean, double exact_max) {
-    const double c = std::ceil(mean + 8.0 * std::sqrt(mean) + 256.0);
-    return (uint32_t)std::min(c, exact_max);
+// Entries per round from rank p to rank q are bounded by the mean + 8 sigma of their (binomial)
+// distribution, or the exact maximum when that is smaller: an overflow is reported, never dropped.
+// Per sub-segment (kSub of them, sub = sender block % kSub): a sub-segment sees about mean / kSub
+// entries; its variance also carries the static spread of which links fall into it, hence the
+// doubled variance.  Never above the exact maximum.
+uint32_t entry_cap_sub(double mean, double exact_max) {
+    const double m = mean / (double)kSub;
+    const double c = std::ceil(m + 8.0 * std::sqrt(2.0 * m) + 64.0);
+    return (uint32_t)std::max(1.0, std::min(c, exact_max));
 }
 
 Chunk chunk_layout(const Handle* h, int p, int q) {
@@ -626,11 +637,11 @@ Chunk chunk_layout(const Handle* h, int p, int q) {
                 const uint32_t m = presence(h->g, (uint32_t)u);
                 if (m) mean += 1.0 / (double)__builtin_popcount(m);
             }
-            c.hcap = std::max<uint32_t>(1u, entry_cap(mean, (double)c.halo));
+            c.hcap = entry_cap_sub(mean, (double)c.halo);
             c.hslot = off;
-            off = align_up(off + (size_t)c.hcap * sizeof(uint32_t));
+            off = align_up(off + (size_t)kSub * c.hcap * sizeof(uint32_t));
             c.hmsg = off;
-            off = align_up(off + (size_t)c.hcap * sizeof(double2));
+            off = align_up(off + (size_t)kSub * c.hcap * sizeof(double2));
         }
     }
     double mean = 0.0, exact = 0.0;
@@ -646,13 +657,13 @@ Chunk chunk_layout(const Handle* h, int p, int q) {
             exact += n;
         }
     }
-    c.cap = entry_cap(mean, exact);
+    c.cap = entry_cap_sub(mean, exact);
     if (exact == 0.0) c.cap = 0;
     c.slot = off;
-    off = align_up(off + (size_t)c.cap * sizeof(uint32_t));
+    off = align_up(off + (size_t)kSub * c.cap * sizeof(uint32_t));
     if (!h->gossip) {
         c.msg = off;
-        off = align_up(off + (size_t)c.cap * sizeof(double2));
+        off = align_up(off + (size_t)kSub * c.cap * sizeof(double2));
     }
     c.size = off;
     return c;
@@ -680,7 +691,7 @@ int build_plan(Handle* h) {
     h->send_total = so;
     h->recv_total = ro;
     int rc;
-    if ((rc = h->alloc(&h->pcount, (size_t)W + 2)) || (rc = h->alloc(&h->overflow, 1)) || (rc = h->alloc(&h->self_newly, 1)))
+    if ((rc = h->alloc(&h->pcount, ((size_t)W + 2) * kSub * kCtrStride)) || (rc = h->alloc(&h->overflow, 1)) || (rc = h->alloc(&h->self_newly, 1)))
         return rc;
     return GP_OK;
 }
@@ -792,7 +803,7 @@ int shard_deliver(Handle* h, const void* recv) {
     // the halo faces (rank-1's last actors land below lo, rank+1's first at hi) and the link
     // entries are applied by one kernel
     const Xchg x = make_xchg(h, h->pending_send, recv);
-    launch_shard_unpack(h->args((uint32_t)k), x, applied_round(h, k), std::max(h->max_in_cap, h->halo),
+    launch_shard_unpack(h->args((uint32_t)k), x, applied_round(h, k), std::max(kSub * h->max_in_cap, h->halo),
                         h->gossip ? 1 : 0, h->full ? 1 : 0, h->stream);
     HIP_TRY(hipGetLastError());
     h->awaiting_deliver = false;

@@ -10,6 +10,11 @@ constexpr int kParts = 64;          // completion sub-counters per round (one 64
 constexpr int kPartStride = 16;     // u32 words between sub-counters
 constexpr int kPartRing = 4;        // rounds kept in the sub-counter ring
 constexpr int kMaxWorld = 16;
+// Exchange entries to one peer are appended into kSub sub-segments (sub = blockIdx % kSub), each
+// with its own counter on its own 128 B line: same-address atomics serialise in L2 (measured at
+// 8 loopback shards: one counter per peer cost 8.5 ms per round).
+constexpr uint32_t kSub = 16;
+constexpr uint32_t kCtrStride = 32;  // u32 words between counters
 
 // One synchronous round kernel F(r) fuses phase 2 of round r-1 (collect the messages sent to
 // this actor, read from the round r-1 buffers) with phase 1 of round r (update, convergence
@@ -45,6 +50,9 @@ struct RoundArgs {
     // push-sum state
     const double2* msg_prev;  // message emitted in round r-1 (= held S,W when not converged)
     double2* msg_cur;
+    // shards (world > 1): link messages of remote senders, by CSR slot (written by the exchange)
+    const double2* rmsg_prev;
+    double2* rmsg_cur;
     const uint8_t* dir_prev;  // direction code of that message (kDirNone: none)
     uint8_t* dir_cur;
     uint8_t* flags;           // termRound (bits 0-3) | converged (bit 4)
@@ -65,17 +73,18 @@ struct RoundArgs {
 
 // Shard exchange (gp_shard_*).  Send chunk to peer q (built by this rank) and receive chunk from
 // peer q (built by q for this rank) share one layout: a 256-byte header; when q is a z-neighbour
-// (rank +-1) the halo face: the direction bytes of the face plane, then (push-sum) `hcap` halo
-// entries, u32 face offsets then (s, w) pairs, for the messages that cross the face only; then
-// `cap` link entries: u32 slot (global link-CSR slot; gossip: slot | (chains-1) << 31; full
-// gossip: the target actor), then push-sum (s, w) pairs.  See DESIGN.md §6.
+// (rank +-1) the halo face: the direction bytes of the face plane, then (push-sum) kSub x `hcap`
+// halo entries, u32 face offsets then (s, w) pairs, for the messages that cross the face only;
+// then kSub x `cap` link entries: u32 slot (global link-CSR slot; gossip: slot | (chains-1) << 31;
+// full gossip: the target actor), then push-sum (s, w) pairs.  See DESIGN.md §6.
 struct ShardHeader {
     unsigned long long newly;  // actors that reported in the round (sender's range)
-    uint32_t nlinks;           // link entries written (<= cap)
     uint32_t overflow;         // sender dropped entries: the run is void (GP_EOVERFLOW)
-    uint32_t nhalo;            // halo entries written (<= hcap)
     uint32_t pad;
+    uint32_t nlinks[kSub];     // link entries written per sub-segment (<= cap)
+    uint32_t nhalo[kSub];      // halo entries written per sub-segment (<= hcap)
 };
+static_assert(sizeof(ShardHeader) <= 256, "the chunk header is 256 bytes");
 
 struct PeerOut {
     ShardHeader* hdr;
@@ -94,7 +103,7 @@ struct PeerIn {
 // The halo faces of a shard, side 0 = rank-1 (this rank's first plane / the halo below lo),
 // side 1 = rank+1 (last plane / the halo from hi).  n == 0: no such neighbour.
 struct HaloX {
-    uint32_t out_first[2], out_n[2], out_cap[2];  // face actors sent (global ids), entry capacity
+    uint32_t out_first[2], out_n[2], out_cap[2];  // face actors sent (global ids), entries per sub-segment
     uint32_t in_first[2], in_n[2], in_cap[2];     // halo rows received
     uint32_t code[2];                             // direction code that crosses the face
     uint8_t* out_dir[2];
@@ -110,8 +119,8 @@ struct Xchg {
     uint32_t world, rank;
     uint32_t abnd[kMaxWorld + 1];  // actor range of every rank
     uint32_t sbnd[kMaxWorld + 1];  // link-slot range of every rank (global CSR numbering)
-    uint32_t* pcount;              // per-peer entry counters of the current round, then the two halo
-                                   // entry counters (zeroed by pack)
+    uint32_t* pcount;              // entry counters of the current round, (peer, sub) then (world +
+                                   // halo side, sub), kCtrStride apart (zeroed by pack)
     uint32_t* overflow;            // sticky local overflow flag
     unsigned long long* self_newly;  // this rank's count of the round (pack -> unpack)
     PeerOut out[kMaxWorld];

@@ -154,8 +154,8 @@ constexpr uint32_t kLinkUnroll = 4;
 // six neighbours' direction bytes, the CSR range; (2) the first 3 grid hits' messages and, per
 // CSR slot of the first kLinkUnroll, the source id and link count (coalesced: CSR order);
 // (3) the messages of the links that fired.
-// LM: 0 no extra links; 1 links.  A shard's remote link senders are no different: the exchange
-// writes their (s, w) into their own (global) rows of msg and marks their CSR slots.
+// LM: 0 no extra links; 1 links; 2 links on a shard of several ranks: a sender outside [lo, hi)
+// is remote, and the exchange wrote its message into the receiver's slot, rmsg_prev[slot].
 template <int LM>
 __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
     if (gate(a, a.r)) return;
@@ -233,7 +233,8 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) {
                     lk[k] = k < nl && lc[k] != 0;
                     if (lk[k]) a.lcnt_prev[li + k] = 0;
-                    lm[k] = load_sel(a.msg_prev, lk[k], ls[k], v);
+                    if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) lm[k] = a.rmsg_prev[li + k];
+                    else lm[k] = load_sel(a.msg_prev, lk[k], ls[k], v);
                 }
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k)
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
                         const uint32_t u = a.rev_src[li + k];
                         a.lcnt_prev[li + k] = 0;
                         flush(u);
-                        add(a.msg_prev[u]);
+                        add(LM == 2 && (u < a.lo || u >= a.hi) ? a.rmsg_prev[li + k] : a.msg_prev[u]);
                     }
                 }
             }
@@ -375,8 +376,14 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// Position of this lane's entry in peer q's send chunk: one atomic per distinct peer per wave
-// (ballot + mbcnt), not one per entry.  Every active lane of the wave must call it.
+__device__ __forceinline__ uint32_t* ctr_at(const Xchg& x, uint32_t q, uint32_t sub) {
+    return x.pcount + (q * kSub + sub) * kCtrStride;
+}
+
+__device__ __forceinline__ uint32_t my_sub() { return blockIdx.x % kSub; }
+
+// Position of this lane's entry in its sub-segment of peer q's send chunk: one atomic per distinct
+// peer per wave (ballot + mbcnt), not one per entry.  Every active lane of the wave must call it.
 __device__ __forceinline__ uint32_t reserve(const Xchg& x, bool want, uint32_t q) {
     unsigned long long pending = __ballot(want);
     uint32_t pos = 0;
@@ -386,7 +393,7 @@ __device__ __forceinline__ uint32_t reserve(const Xchg& x, bool want, uint32_t q
         const bool mine = want && q == qq;
         const unsigned long long mask = __ballot(mine);
         uint32_t base = 0;
-        if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(&x.pcount[qq], (uint32_t)__popcll(mask));
+        if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(ctr_at(x, qq, my_sub()), (uint32_t)__popcll(mask));
         base = __shfl(base, leader, 64);
         if (mine) pos = base + lanes_below(mask);
         pending &= ~mask;
@@ -394,14 +401,36 @@ __device__ __forceinline__ uint32_t reserve(const Xchg& x, bool want, uint32_t q
     return pos;
 }
 
-// Append (entry, msg) to peer q's chunk at pos, or flag the overflow (never silently dropped:
-// gp_shard_sync fails the run with GP_EOVERFLOW).
+// Positions of K entries per thread in their peers' chunks, reserved per BLOCK: LDS counters per
+// peer, then one global atomic per (block, peer) on the block's sub-segment counter.  At 8 ranks
+// ~7/8 of the link messages are remote: per-wave reservation on one counter per peer cost 8.5 ms
+// per round (8 loopback shards of 80M actors).  Every thread of the block must call it.
+template <uint32_t K>
+__device__ __forceinline__ void block_reserve(const Xchg& x, const bool (&want)[K], const uint32_t (&q)[K],
+                                              uint32_t (&pos)[K]) {
+    __shared__ uint32_t cnt[kMaxWorld], base[kMaxWorld];
+    if (threadIdx.x < kMaxWorld) cnt[threadIdx.x] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < K; ++j) pos[j] = want[j] ? atomicAdd(&cnt[q[j]], 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x < x.world && cnt[threadIdx.x])
+        base[threadIdx.x] = atomicAdd(ctr_at(x, threadIdx.x, my_sub()), cnt[threadIdx.x]);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < K; ++j)
+        if (want[j]) pos[j] += base[q[j]];
+}
+
+// Append (entry, msg) to peer q's chunk, sub-segment my_sub(), at pos, or flag the overflow (never
+// silently dropped: gp_shard_sync fails the run with GP_EOVERFLOW).
 template <bool MSG>
 __device__ __forceinline__ void put(const Xchg& x, uint32_t q, uint32_t pos, uint32_t entry, double2 m) {
     const PeerOut& o = x.out[q];
     if (pos < o.cap) {
-        o.slot[pos] = entry;
-        if (MSG) o.msg[pos] = m;
+        const uint32_t i = my_sub() * o.cap + pos;
+        o.slot[i] = entry;
+        if (MSG) o.msg[i] = m;
     } else {
         atomicOr(x.overflow, 1u);
     }
@@ -432,14 +461,16 @@ __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg 
         rm[j] = l[j] && (lp[j] < slo || lp[j] >= shi);
         mm[j] = load_sel(a.msg_cur, rm[j], base + j * kBlock, a.lo);
     }
+    uint32_t q[kScatterPer], pos[kScatterPer];
 #pragma unroll
     for (uint32_t j = 0; j < kScatterPer; ++j) {
-        const bool remote = rm[j];
-        if (l[j] && !remote) a.lcnt_cur[lp[j]] = 1;
-        const uint32_t q = remote ? owner(x.sbnd, x.world, lp[j]) : 0u;
-        const uint32_t pos = reserve(x, remote, q);
-        if (remote) put<true>(x, q, pos, lp[j], mm[j]);
+        if (l[j] && !rm[j]) a.lcnt_cur[lp[j]] = 1;
+        q[j] = rm[j] ? owner(x.sbnd, x.world, lp[j]) : 0u;
     }
+    block_reserve(x, rm, q, pos);
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j)
+        if (rm[j]) put<true>(x, q[j], pos[j], lp[j], mm[j]);
 }
 
 __global__ __launch_bounds__(kBlock) void k_gs_link_scatter_x(RoundArgs a, Xchg x) {
@@ -455,14 +486,18 @@ __global__ __launch_bounds__(kBlock) void k_gs_link_scatter_x(RoundArgs a, Xchg 
     }
 #pragma unroll
     for (uint32_t j = 0; j < kScatterPer; ++j) lp[j] = load_sel(a.lpos, nl[j] != 0u, base + j * kBlock, a.lo);
+    bool rm[kScatterPer];
+    uint32_t q[kScatterPer], pos[kScatterPer];
 #pragma unroll
     for (uint32_t j = 0; j < kScatterPer; ++j) {
-        const bool remote = nl[j] && (lp[j] < slo || lp[j] >= shi);
-        if (nl[j] && !remote) a.lcnt_cur[lp[j]] = (uint8_t)nl[j];
-        const uint32_t q = remote ? owner(x.sbnd, x.world, lp[j]) : 0u;
-        const uint32_t pos = reserve(x, remote, q);
-        if (remote) put<false>(x, q, pos, lp[j] | ((nl[j] - 1u) << 31), make_double2(0.0, 0.0));
+        rm[j] = nl[j] && (lp[j] < slo || lp[j] >= shi);
+        if (nl[j] && !rm[j]) a.lcnt_cur[lp[j]] = (uint8_t)nl[j];
+        q[j] = rm[j] ? owner(x.sbnd, x.world, lp[j]) : 0u;
     }
+    block_reserve(x, rm, q, pos);
+#pragma unroll
+    for (uint32_t j = 0; j < kScatterPer; ++j)
+        if (rm[j]) put<false>(x, q[j], pos[j], lp[j] | ((nl[j] - 1u) << 31), make_double2(0.0, 0.0));
 }
 
 // Halo faces of F(k), after the round kernel: the direction bytes of this rank's first plane go
@@ -470,14 +505,17 @@ __global__ __launch_bounds__(kBlock) void k_gs_link_scatter_x(RoundArgs a, Xchg 
 // those that cross the face (about 1/7 of the plane) as (face offset, s, w) entries.  The
 // receiver's halo rows keep stale messages elsewhere; its pull kernel reads a halo message only
 // when the direction byte points across, so they are never read.
-__device__ __forceinline__ uint32_t reserve1(uint32_t* ctr, bool want) {
-    const unsigned long long mask = __ballot(want);
-    if (!mask) return 0u;
-    const int leader = __ffsll((long long)mask) - 1;
-    uint32_t base = 0;
-    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(ctr, (uint32_t)__popcll(mask));
-    base = __shfl(base, leader, 64);
-    return base + lanes_below(mask);
+// Block-aggregated position on one counter (LDS first, then one global atomic per block).
+// Every thread of the block must call it.
+__device__ __forceinline__ uint32_t block_reserve1(uint32_t* ctr, bool want) {
+    __shared__ uint32_t cnt, base;
+    if (threadIdx.x == 0) cnt = 0u;
+    __syncthreads();
+    uint32_t pos = want ? atomicAdd(&cnt, 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x == 0 && cnt) base = atomicAdd(ctr, cnt);
+    __syncthreads();
+    return pos + (want ? base : 0u);
 }
 
 __global__ __launch_bounds__(kBlock) void k_shard_halo(RoundArgs a, Xchg x, int pushsum) {
@@ -487,7 +525,8 @@ __global__ __launch_bounds__(kBlock) void k_shard_halo(RoundArgs a, Xchg x, int 
         uint8_t* odir = x.h.out_dir[side];
         uint32_t* oslot = x.h.out_slot[side];
         double2* omsg = x.h.out_msg[side];
-        uint32_t* ctr = x.pcount + x.world + side;
+        uint32_t* ctr = ctr_at(x, x.world + side, my_sub());
+        const uint32_t seg = my_sub() * cap;
         // block-uniform trip count: every lane of a wave reaches reserve1
         for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
             const uint32_t i = base + threadIdx.x;
@@ -497,11 +536,11 @@ __global__ __launch_bounds__(kBlock) void k_shard_halo(RoundArgs a, Xchg x, int 
             const bool cross = pushsum && valid && b == code;
             double2 m = make_double2(0.0, 0.0);
             if (pushsum) m = load_sel(a.msg_cur, cross, first + i, first);  // gossip: no msg array
-            const uint32_t pos = reserve1(ctr, cross);
+            const uint32_t pos = block_reserve1(ctr, cross);
             if (cross) {
                 if (pos < cap) {
-                    oslot[pos] = i;
-                    omsg[pos] = m;
+                    oslot[seg + pos] = i;
+                    omsg[seg + pos] = m;
                 } else {
                     atomicOr(x.overflow, 1u);
                 }
@@ -510,32 +549,44 @@ __global__ __launch_bounds__(kBlock) void k_shard_halo(RoundArgs a, Xchg x, int 
     }
 }
 
-// Round `applied`'s count into every send header; the per-peer counters restart at 0.
+// Round `applied`'s count into every send header; the entry counters restart at 0.  One wave:
+// lane s < kSub handles sub-segment s of every peer.
 __global__ void k_shard_pack(RoundArgs a, Xchg x, long long applied) {
     unsigned long long newly = 0;
     if (applied >= 0) newly = *part_slot(a.parts, applied, threadIdx.x);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) newly += __shfl_xor(newly, off, 64);
     if (threadIdx.x == 0) *x.self_newly = newly;
-    const uint32_t q = threadIdx.x;
-    if (q < x.world && q != x.rank) {
-        const uint32_t c = x.pcount[q];
-        ShardHeader h;
-        h.newly = newly;
-        h.nlinks = c < x.out[q].cap ? c : x.out[q].cap;
-        h.overflow = (c > x.out[q].cap || *x.overflow) ? 1u : 0u;
-        h.nhalo = 0u;
-        h.pad = 0u;
-        const int side = q + 1 == x.rank ? 0 : q == x.rank + 1 ? 1 : -1;
-        if (side >= 0) {
-            uint32_t* hc = x.pcount + x.world + side;
-            const uint32_t n = *hc;
-            h.nhalo = n < x.h.out_cap[side] ? n : x.h.out_cap[side];
-            if (n > x.h.out_cap[side]) h.overflow = 1u;
-            *hc = 0u;
+    const uint32_t s = threadIdx.x;
+    const bool lane = s < kSub;
+    const uint32_t local_of = *x.overflow;
+    for (uint32_t q = 0; q < x.world; ++q) {
+        if (q == x.rank) continue;
+        ShardHeader* hd = x.out[q].hdr;
+        bool of = false;
+        if (lane) {
+            uint32_t* lc = ctr_at(x, q, s);
+            const uint32_t c = *lc;
+            hd->nlinks[s] = c < x.out[q].cap ? c : x.out[q].cap;
+            of = c > x.out[q].cap;
+            *lc = 0u;
+            const int side = q + 1 == x.rank ? 0 : q == x.rank + 1 ? 1 : -1;
+            uint32_t nh = 0;
+            if (side >= 0) {
+                uint32_t* hc = ctr_at(x, x.world + side, s);
+                const uint32_t n = *hc;
+                nh = n < x.h.out_cap[side] ? n : x.h.out_cap[side];
+                of = of || n > x.h.out_cap[side];
+                *hc = 0u;
+            }
+            hd->nhalo[s] = nh;
         }
-        *x.out[q].hdr = h;
-        x.pcount[q] = 0u;
+        const unsigned long long any = __ballot(of);
+        if (threadIdx.x == 0) {
+            hd->newly = newly;
+            hd->overflow = (any || local_of) ? 1u : 0u;
+            hd->pad = 0u;
+        }
     }
 }
 
@@ -562,15 +613,18 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
         const uint8_t* idir = x.h.in_dir[side];
         for (uint32_t i = gtid; i < n; i += gstride) a.dir_cur[first + i] = idir[i];
         if (!x.h.in_slot[side]) continue;
-        uint32_t ne = x.h.in_hdr[side]->nhalo;
-        ne = ne < x.h.in_cap[side] ? ne : x.h.in_cap[side];
-        for (uint32_t i = gtid; i < ne; i += gstride) {
-            const uint32_t o = x.h.in_slot[side][i];
-            if (o >= n) {
-                atomicOr(x.overflow, 2u);
-                continue;
+        const uint32_t cap = x.h.in_cap[side];
+        for (uint32_t sb = 0; sb < kSub; ++sb) {
+            uint32_t ne = x.h.in_hdr[side]->nhalo[sb];
+            ne = ne < cap ? ne : cap;
+            for (uint32_t i = sb * cap + gtid; i < sb * cap + ne; i += gstride) {
+                const uint32_t o = x.h.in_slot[side][i];
+                if (o >= n) {
+                    atomicOr(x.overflow, 2u);
+                    continue;
+                }
+                a.msg_cur[first + o] = x.h.in_msg[side][i];
             }
-            a.msg_cur[first + o] = x.h.in_msg[side][i];
         }
     }
     // an entry outside this rank's actors / slots can only come from a corrupt chunk: it is
@@ -579,9 +633,11 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
     for (uint32_t q = 0; q < x.world; ++q) {
         if (q == x.rank) continue;
         const PeerIn& in = x.in[q];
-        uint32_t n = in.hdr->nlinks;
-        n = n < in.cap ? n : in.cap;
-        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        if (!in.cap) continue;
+        // kSub sub-segments of `cap` entries; entries past a sub-segment's count are unused
+        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < kSub * in.cap; i += gridDim.x * kBlock) {
+            const uint32_t sb = i / in.cap;
+            if (i - sb * in.cap >= in.hdr->nlinks[sb]) continue;
             const uint32_t e = in.slot[i];
             const uint32_t t = (gossip && !full) ? e & 0x7FFFFFFFu : e;
             if (t < elo || t >= ehi) {
@@ -590,8 +646,8 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
             }
             if (full) atomicAdd(&a.inc_cur[t], 1u);
             else if (gossip) a.lcnt_cur[t] = (uint8_t)((e >> 31) + 1u);
-            else {  // the sender's message into its own row; its slot marked for the receiver
-                a.msg_cur[a.rev_src[t]] = in.msg[i];
+            else {  // the sender's message into the receiver's slot, the slot marked
+                a.rmsg_cur[t] = in.msg[i];
                 a.lcnt_cur[t] = 1;
             }
         }
@@ -946,6 +1002,7 @@ uint32_t span_for(uint32_t n, int grid) {
 
 void launch_ps_pull(const RoundArgs& a, const Launch& l) {
     if (!a.g.has_link) hipLaunchKernelGGL(k_ps_pull<0>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+    else if (a.rmsg_prev) hipLaunchKernelGGL(k_ps_pull<2>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
     else hipLaunchKernelGGL(k_ps_pull<1>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
 }
 
@@ -1001,9 +1058,9 @@ void launch_shard_pack(const RoundArgs& a, const Xchg& x, long long applied, hip
     hipLaunchKernelGGL(k_shard_pack, dim3(1), dim3(64), 0, s, a, x, applied);
 }
 
-void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, uint32_t max_cap, int gossip,
+void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, uint32_t max_entries, int gossip,
                          int full, hipStream_t s) {
-    uint32_t blocks = (max_cap + kBlock - 1) / kBlock;
+    uint32_t blocks = (max_entries + kBlock - 1) / kBlock;
     blocks = blocks < 1u ? 1u : (blocks > (uint32_t)kMaxGrid ? (uint32_t)kMaxGrid : blocks);
     hipLaunchKernelGGL(k_shard_unpack, dim3(blocks), dim3(kBlock), 0, s, a, x, applied, gossip, full);
 }
