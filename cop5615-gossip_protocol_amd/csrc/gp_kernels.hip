@@ -614,28 +614,28 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
         for (uint32_t i = gtid; i < n; i += gstride) a.dir_cur[first + i] = idir[i];
         if (!x.h.in_slot[side]) continue;
         const uint32_t cap = x.h.in_cap[side];
-        for (uint32_t sb = 0; sb < kSub; ++sb) {
-            uint32_t ne = x.h.in_hdr[side]->nhalo[sb];
-            ne = ne < cap ? ne : cap;
-            for (uint32_t i = sb * cap + gtid; i < sb * cap + ne; i += gstride) {
-                const uint32_t o = x.h.in_slot[side][i];
-                if (o >= n) {
-                    atomicOr(x.overflow, 2u);
-                    continue;
-                }
-                a.msg_cur[first + o] = x.h.in_msg[side][i];
+        for (uint32_t i = gtid; i < kSub * cap; i += gstride) {  // one pass over every sub-segment
+            const uint32_t sb = i / cap;
+            if (i - sb * cap >= x.h.in_hdr[side]->nhalo[sb]) continue;
+            const uint32_t o = x.h.in_slot[side][i];
+            if (o >= n) {
+                atomicOr(x.overflow, 2u);
+                continue;
             }
+            a.msg_cur[first + o] = x.h.in_msg[side][i];
         }
     }
     // an entry outside this rank's actors / slots can only come from a corrupt chunk: it is
     // reported (GP_EOVERFLOW at the next sync), never written
     const uint32_t elo = full ? a.lo : x.sbnd[x.rank], ehi = full ? a.hi : x.sbnd[x.rank + 1];
-    for (uint32_t q = 0; q < x.world; ++q) {
-        if (q == x.rank) continue;
+    // the grid is world x bpp blocks: block b serves peer b / bpp, so the peers' entries are in
+    // flight together (one peer after another left each thread a chain of dependent loads per peer)
+    const uint32_t bpp = gridDim.x / x.world;
+    const uint32_t q = blockIdx.x / bpp;
+    if (q < x.world && q != x.rank && x.in[q].cap) {
         const PeerIn& in = x.in[q];
-        if (!in.cap) continue;
         // kSub sub-segments of `cap` entries; entries past a sub-segment's count are unused
-        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < kSub * in.cap; i += gridDim.x * kBlock) {
+        for (uint32_t i = (blockIdx.x % bpp) * kBlock + threadIdx.x; i < kSub * in.cap; i += bpp * kBlock) {
             const uint32_t sb = i / in.cap;
             if (i - sb * in.cap >= in.hdr->nlinks[sb]) continue;
             const uint32_t e = in.slot[i];
@@ -1060,9 +1060,10 @@ void launch_shard_pack(const RoundArgs& a, const Xchg& x, long long applied, hip
 
 void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, uint32_t max_entries, int gossip,
                          int full, hipStream_t s) {
-    uint32_t blocks = (max_entries + kBlock - 1) / kBlock;
-    blocks = blocks < 1u ? 1u : (blocks > (uint32_t)kMaxGrid ? (uint32_t)kMaxGrid : blocks);
-    hipLaunchKernelGGL(k_shard_unpack, dim3(blocks), dim3(kBlock), 0, s, a, x, applied, gossip, full);
+    const uint32_t cap = (uint32_t)kMaxGrid / x.world;
+    uint32_t bpp = (max_entries + kBlock - 1) / kBlock;
+    bpp = bpp < 1u ? 1u : (bpp > cap ? cap : bpp);
+    hipLaunchKernelGGL(k_shard_unpack, dim3(bpp * x.world), dim3(kBlock), 0, s, a, x, applied, gossip, full);
 }
 
 void launch_link_hist(const uint32_t* link, const Geom& g, const Xchg& x, unsigned long long* hist,
