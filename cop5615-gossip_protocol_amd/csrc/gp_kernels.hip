@@ -372,34 +372,12 @@ __device__ __forceinline__ uint32_t owner(const uint32_t* b, uint32_t world, uin
     return q;
 }
 
-__device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
 
 __device__ __forceinline__ uint32_t* ctr_at(const Xchg& x, uint32_t q, uint32_t sub) {
     return x.pcount + (q * kSub + sub) * kCtrStride;
 }
 
 __device__ __forceinline__ uint32_t my_sub() { return blockIdx.x % kSub; }
-
-// Position of this lane's entry in its sub-segment of peer q's send chunk: one atomic per distinct
-// peer per wave (ballot + mbcnt), not one per entry.  Every active lane of the wave must call it.
-__device__ __forceinline__ uint32_t reserve(const Xchg& x, bool want, uint32_t q) {
-    unsigned long long pending = __ballot(want);
-    uint32_t pos = 0;
-    while (pending) {
-        const int leader = __ffsll((long long)pending) - 1;
-        const uint32_t qq = __shfl(q, leader, 64);
-        const bool mine = want && q == qq;
-        const unsigned long long mask = __ballot(mine);
-        uint32_t base = 0;
-        if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(ctr_at(x, qq, my_sub()), (uint32_t)__popcll(mask));
-        base = __shfl(base, leader, 64);
-        if (mine) pos = base + lanes_below(mask);
-        pending &= ~mask;
-    }
-    return pos;
-}
 
 // Positions of K entries per thread in their peers' chunks, reserved per BLOCK: LDS counters per
 // peer, then one global atomic per (block, peer) on the block's sub-segment counter.  At 8 ranks
@@ -694,26 +672,29 @@ __device__ __forceinline__ void gs_push_body(const RoundArgs& a, const Xchg* xp)
     uint32_t v, end, step;
     node_range(a.lo, a.hi, a.span, v, end, step);
     uint32_t newly = 0;
-    for (; v < end; v += step) {
-        uint32_t m;
-        const uint32_t d = generic_deg(a, v, m);
-        if (!d) continue;
-        const uint8_t st = a.gstate[v];
-        uint32_t tok = st & 3u;
-        uint32_t done = (st >> 2) & 1u;
-        if (r) {
-            const uint32_t inc = a.inc_prev[v];
-            if (inc) {
-                a.inc_prev[v] = 0;
-                if (!done) {
-                    const uint32_t c0 = a.cnt[v], c1 = c0 + inc;
-                    a.cnt[v] = c1;
-                    if (c0 == 0) ++tok;
-                    if (c0 <= a.threshold && c1 > a.threshold) {
-                        done = 1;
-                        ++newly;
+    // X: the walk is block-uniform (block_reserve synchronises the block); lanes past the end idle
+    for (; X ? v - threadIdx.x < end : v < end; v += step) {
+        uint32_t m = 0, d = 0;
+        if (!X || v < end) d = generic_deg(a, v, m);
+        uint32_t tok = 0;
+        if (d) {
+            const uint8_t st = a.gstate[v];
+            tok = st & 3u;
+            uint32_t done = (st >> 2) & 1u;
+            if (r) {
+                const uint32_t inc = a.inc_prev[v];
+                if (inc) {
+                    a.inc_prev[v] = 0;
+                    if (!done) {
+                        const uint32_t c0 = a.cnt[v], c1 = c0 + inc;
+                        a.cnt[v] = c1;
+                        if (c0 == 0) ++tok;
+                        if (c0 <= a.threshold && c1 > a.threshold) {
+                            done = 1;
+                            ++newly;
+                        }
+                        a.gstate[v] = (uint8_t)(tok | (done << 2));
                     }
-                    a.gstate[v] = (uint8_t)(tok | (done << 2));
                 }
             }
         }
@@ -731,15 +712,19 @@ __device__ __forceinline__ void gs_push_body(const RoundArgs& a, const Xchg* xp)
                 t[0] = generic_target(a, v, m, scale_draw(px.x, d));
                 t[1] = generic_target(a, v, m, scale_draw(px.y, d));
             }
+            bool remote[2];
+            uint32_t q[2], pos[2];
 #pragma unroll
             for (uint32_t c = 0; c < 2; ++c) {
                 const bool send = tok > c;
-                const bool remote = send && (t[c] < a.lo || t[c] >= a.hi);
-                if (send && !remote) atomicAdd(&a.inc_cur[t[c]], 1u);
-                const uint32_t q = remote ? owner(x.abnd, x.world, t[c]) : 0u;
-                const uint32_t pos = reserve(x, remote, q);
-                if (remote) put<false>(x, q, pos, t[c], make_double2(0.0, 0.0));
+                remote[c] = send && (t[c] < a.lo || t[c] >= a.hi);
+                if (send && !remote[c]) atomicAdd(&a.inc_cur[t[c]], 1u);
+                q[c] = remote[c] ? owner(x.abnd, x.world, t[c]) : 0u;
             }
+            block_reserve(x, remote, q, pos);
+#pragma unroll
+            for (uint32_t c = 0; c < 2; ++c)
+                if (remote[c]) put<false>(x, q[c], pos[c], t[c], make_double2(0.0, 0.0));
         }
     }
     if (r) block_add(newly, a.parts, (long long)r - 1);
