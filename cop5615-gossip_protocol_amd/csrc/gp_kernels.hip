@@ -255,8 +255,14 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
         }
         const uint8_t f0 = f;
         const PsOut o = ps_update(f, held, ss, ww, cin, a.delta, a.term_limit);
-        if (o.send) a.msg_cur[v] = o.msg;
-        a.dir_cur[v] = o.send ? (uint8_t)code : kDirNone;
+        // non-temporal: the round's 160 MB of messages cannot stay in L2 until the next round
+        // reads them, and streaming them past it leaves L2 to the +-G, +-G^2 rows read now
+        // (measured ~1.5% per round; non-temporal LOADS of the CSR were 7% slower)
+        if (o.send) {
+            __builtin_nontemporal_store(o.msg.x, &a.msg_cur[v].x);
+            __builtin_nontemporal_store(o.msg.y, &a.msg_cur[v].y);
+        }
+        __builtin_nontemporal_store(o.send ? (uint8_t)code : kDirNone, &a.dir_cur[v]);
         if (f != f0) a.flags[v] = f;
         if (o.conv_now) {
             a.frozen[v] = o.msg;
