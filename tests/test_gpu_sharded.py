@@ -101,6 +101,26 @@ def test_shards_vs_single_gpu_100k(n, topo, algo, world, rounds):
     _check_vs(ref, engines, algo)
 
 
+@pytest.mark.parametrize("n,topo,algo,rounds", [
+    (2_000_000, "Imp3D", "push-sum", None),   # 7/8 of the links remote, both halo sides
+    (1_000_000, "3D", "push-sum", 400),
+    (1_000_000, "full", "gossip", None),      # every receipt an entry, 7 peers
+    (1_000_000, "Imp3D", "gossip", None),
+])
+def test_shards_vs_single_gpu_world8(n, topo, algo, rounds):
+    """The driver's 8-rank layout (8 shards on one GPU, loopback exchange): every peer's
+    sub-segments, the owner() search over 8 bounds and the middle ranks' two halo faces, bit
+    for bit against the single-GPU engine."""
+    cap = rounds or 1 << 30
+    ref = Simulator(n, topo, algo, seed=7)
+    rs = ref.step(cap)
+    engines = _shards(n, topo, algo, 8, seed=7)
+    sts = sharded.run_local(engines, max_rounds=cap)
+    assert (sts[0].round, sts[0].completed, sts[0].converged) == (rs.round, rs.completed, rs.converged)
+    np.testing.assert_array_equal(engines[0].read_trace(), ref.read_trace())
+    _check_vs(ref, engines, algo)
+
+
 def test_shards_imp3d_10m_two_ranks():
     """BASELINE config 3 split over 2 shards: the same run as the single-GPU engine."""
     ref = Simulator(10_000_000, "Imp3D", "push-sum", seed=1)
