@@ -1,6 +1,7 @@
 // gossip_cli.cpp — drop-in replacement for the reference's program entry point.
 //
 //   gossip numNodes topology algorithm [--seed S] [--max-rounds R] [--device D] [--quiet]
+//          [--trace FILE]
 //
 // Same positional contract as /root/reference/program.fs:19-21 (argv[1] = numNodes,
 // argv[2] = topology "line" | "full" | "2D" | "Imp3D" (+ build-defined "3D"), argv[3] =
@@ -11,10 +12,15 @@
 // Deliberate deviations: an invalid algorithm or topology exits with status 2
 // instead of hanging at Console.ReadLine() (program.fs:188-189, 331-334); a run that hits
 // --max-rounds without converging exits with status 3.
+//
+// --trace FILE writes the ParentActor's count after every round as CSV (round,completed): the
+// convergence curve behind report.pdf p.3-4, at any size.
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "gossip_hip.h"
 
@@ -38,7 +44,8 @@ const char* banner(int topo, int algo) {
 
 int main(int argc, char** argv) {
     if (argc < 4) {
-        std::fprintf(stderr, "usage: %s numNodes topology algorithm [--seed S] [--max-rounds R] [--device D]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s numNodes topology algorithm [--seed S] [--max-rounds R] [--device D] [--quiet] [--trace FILE]\n",
+                     argv[0]);
         return 2;
     }
     gp_config cfg{};
@@ -51,12 +58,14 @@ int main(int argc, char** argv) {
     cfg.term_limit = 3;
     long long max_rounds = 1LL << 40;
     bool quiet = false;
+    const char* trace_path = nullptr;
     for (int i = 4; i < argc; ++i) {
         const std::string a = argv[i];
         if (a == "--seed" && i + 1 < argc) cfg.seed = std::strtoull(argv[++i], nullptr, 10);
         else if (a == "--max-rounds" && i + 1 < argc) max_rounds = std::strtoll(argv[++i], nullptr, 10);
         else if (a == "--device" && i + 1 < argc) cfg.device = std::atoi(argv[++i]);
         else if (a == "--quiet") quiet = true;
+        else if (a == "--trace" && i + 1 < argc) trace_path = argv[++i];
         else {
             std::fprintf(stderr, "unknown option %s\n", a.c_str());
             return 2;
@@ -100,6 +109,19 @@ int main(int argc, char** argv) {
         std::printf("Not converged after %lld rounds (%lld of %lld reported), %f ms\n", (long long)st.round,
                     (long long)st.completed, (long long)lay.nodes, st.device_ms);
         rc = 3;
+    }
+    if (trace_path) {
+        std::vector<int64_t> done((size_t)st.round);
+        FILE* f = std::fopen(trace_path, "w");
+        if (!f || (st.round && gp_read_trace(h, 0, st.round, done.data()) != GP_OK)) {
+            std::fprintf(stderr, "--trace %s: %s\n", trace_path, f ? gp_last_error() : std::strerror(errno));
+            if (f) std::fclose(f);
+            gp_destroy(h);
+            return 1;
+        }
+        std::fprintf(f, "round,completed\n");
+        for (int64_t r = 0; r < st.round; ++r) std::fprintf(f, "%lld,%lld\n", (long long)r, (long long)done[(size_t)r]);
+        std::fclose(f);
     }
     gp_destroy(h);
     return rc;

@@ -146,3 +146,28 @@ def test_invalid_config_errors():
         Simulator(0, "line", "gossip")
     with pytest.raises(GossipError):
         Simulator(10, "line", "gossip", term_limit=0)
+
+
+def test_cli_report_and_trace(tmp_path):
+    """The drop-in CLI (program.fs:19-21 argv, :51-52 report) on the GPU: banner, convergence
+    report and rounds, and --trace's per-round count curve equal to the oracle's."""
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "cop5615-gossip_protocol_amd", "lib", "gossip")
+    out = tmp_path / "trace.csv"
+    r = subprocess.run([exe, "1000", "Imp3D", "push-sum", "--seed", "3", "--trace", str(out)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[0] == "Push Sum Started"  # program.fs:322
+    assert any(x.startswith("Convergence Time: ") and x.endswith(" ms") for x in lines)
+    cpu = oracle.OracleSim(1000, "Imp3D", "push-sum", seed=3)
+    cs = cpu.step()
+    assert f"Rounds: {cs.round}" in lines
+    rows = np.loadtxt(out, delimiter=",", skiprows=1, dtype=np.int64).reshape(-1, 2)
+    np.testing.assert_array_equal(rows[:, 0], np.arange(cs.round))
+    np.testing.assert_array_equal(rows[:, 1], cpu.read_trace())
+    assert rows[-1, 1] == int(cpu.layout.nodes)
+    cpu.close()
