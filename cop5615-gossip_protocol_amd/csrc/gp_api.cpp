@@ -963,12 +963,9 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
             return bail(rc);
         }
     } else {
-        // a sharded Imp3D run keeps message rows for every actor: a remote extra-link sender's
-        // message is written into its own row by the exchange (k_shard_unpack)
-        const bool global_rows = h->sharded && h->g.has_link;
-        const size_t mn = global_rows ? A : xn;
-        const int64_t mlo = global_rows ? 0 : xlo;
-        if ((rc = h->alloc(&h->msg[0], mn, mlo)) || (rc = h->alloc(&h->msg[1], mn, mlo)) ||
+        // message rows for the own actors and both halos; a remote extra-link sender's message
+        // lands in the receiver's CSR slot (rmsg), not in a row of the sender
+        if ((rc = h->alloc(&h->msg[0], xn, xlo)) || (rc = h->alloc(&h->msg[1], xn, xlo)) ||
             (rc = h->alloc(&h->flags, n, lo)) || (rc = h->alloc(&h->frozen, n, lo)) ||
             (rc = h->alloc(&h->partials, (size_t)h->grid)))
             return bail(rc);
