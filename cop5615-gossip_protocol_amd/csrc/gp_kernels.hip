@@ -420,67 +420,71 @@ __device__ __forceinline__ void put(const Xchg& x, uint32_t q, uint32_t pos, uin
     }
 }
 
+// Actors per thread of the sharded link passes (block-strided): more per block means fewer
+// block-level reservations (three barriers and one global atomic per peer each).
+constexpr uint32_t kShardPer = 4;
+
 // Sharded push-sum link pass: a link message whose CSR slot is this rank's gets the slot's link
 // count (the receiver reads msg_prev[u] itself, as on one GPU); one whose slot belongs to another
 // rank goes to that rank's send chunk as (global slot, s, w), written into the same slot there.
 __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg x) {
     const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
-    const uint32_t base = a.lo + blockIdx.x * kBlock * kScatterPer + threadIdx.x;
+    const uint32_t base = a.lo + blockIdx.x * kBlock * kShardPer + threadIdx.x;
     const uint32_t slo = x.sbnd[x.rank], shi = x.sbnd[x.rank + 1];
-    bool l[kScatterPer];
+    bool l[kShardPer];
 #pragma unroll
-    for (uint32_t j = 0; j < kScatterPer; ++j) {
+    for (uint32_t j = 0; j < kShardPer; ++j) {
         const uint32_t u = base + j * kBlock;
         l[j] = u < n && load_sel(a.dir_cur, u < n, u, a.lo) == kDirLink;
     }
-    uint32_t lp[kScatterPer];
+    uint32_t lp[kShardPer];
 #pragma unroll
-    for (uint32_t j = 0; j < kScatterPer; ++j) lp[j] = load_sel(a.lpos, l[j], base + j * kBlock, a.lo);
+    for (uint32_t j = 0; j < kShardPer; ++j) lp[j] = load_sel(a.lpos, l[j], base + j * kBlock, a.lo);
     // only a remote link needs its message: the fired ~1/7 of senders would otherwise pull in
     // ~70% of msg_cur's lines (8 messages per 128 B line)
-    bool rm[kScatterPer];
-    double2 mm[kScatterPer];
+    bool rm[kShardPer];
+    double2 mm[kShardPer];
 #pragma unroll
-    for (uint32_t j = 0; j < kScatterPer; ++j) {
+    for (uint32_t j = 0; j < kShardPer; ++j) {
         rm[j] = l[j] && (lp[j] < slo || lp[j] >= shi);
         mm[j] = load_sel(a.msg_cur, rm[j], base + j * kBlock, a.lo);
     }
-    uint32_t q[kScatterPer], pos[kScatterPer];
+    uint32_t q[kShardPer], pos[kShardPer];
 #pragma unroll
-    for (uint32_t j = 0; j < kScatterPer; ++j) {
+    for (uint32_t j = 0; j < kShardPer; ++j) {
         if (l[j] && !rm[j]) a.lcnt_cur[lp[j]] = 1;
         q[j] = rm[j] ? owner(x.sbnd, x.world, lp[j]) : 0u;
     }
     block_reserve(x, rm, q, pos);
 #pragma unroll
-    for (uint32_t j = 0; j < kScatterPer; ++j)
+    for (uint32_t j = 0; j < kShardPer; ++j)
         if (rm[j]) put<true>(x, q[j], pos[j], lp[j], mm[j]);
 }
 
 __global__ __launch_bounds__(kBlock) void k_gs_link_scatter_x(RoundArgs a, Xchg x) {
     const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
-    const uint32_t base = a.lo + blockIdx.x * kBlock * kScatterPer + threadIdx.x;
+    const uint32_t base = a.lo + blockIdx.x * kBlock * kShardPer + threadIdx.x;
     const uint32_t slo = x.sbnd[x.rank], shi = x.sbnd[x.rank + 1];
-    uint32_t nl[kScatterPer], lp[kScatterPer];
+    uint32_t nl[kShardPer], lp[kShardPer];
 #pragma unroll
-    for (uint32_t j = 0; j < kScatterPer; ++j) {
+    for (uint32_t j = 0; j < kShardPer; ++j) {
         const uint32_t u = base + j * kBlock;
         const uint8_t b = load_sel(a.dir_cur, u < n, u, a.lo);
         nl[j] = u < n ? (uint32_t)((b & 15u) == kDirLink) + (uint32_t)((b >> 4) == kDirLink) : 0u;
     }
 #pragma unroll
-    for (uint32_t j = 0; j < kScatterPer; ++j) lp[j] = load_sel(a.lpos, nl[j] != 0u, base + j * kBlock, a.lo);
-    bool rm[kScatterPer];
-    uint32_t q[kScatterPer], pos[kScatterPer];
+    for (uint32_t j = 0; j < kShardPer; ++j) lp[j] = load_sel(a.lpos, nl[j] != 0u, base + j * kBlock, a.lo);
+    bool rm[kShardPer];
+    uint32_t q[kShardPer], pos[kShardPer];
 #pragma unroll
-    for (uint32_t j = 0; j < kScatterPer; ++j) {
+    for (uint32_t j = 0; j < kShardPer; ++j) {
         rm[j] = nl[j] && (lp[j] < slo || lp[j] >= shi);
         if (nl[j] && !rm[j]) a.lcnt_cur[lp[j]] = (uint8_t)nl[j];
         q[j] = rm[j] ? owner(x.sbnd, x.world, lp[j]) : 0u;
     }
     block_reserve(x, rm, q, pos);
 #pragma unroll
-    for (uint32_t j = 0; j < kScatterPer; ++j)
+    for (uint32_t j = 0; j < kShardPer; ++j)
         if (rm[j]) put<false>(x, q[j], pos[j], lp[j] | ((nl[j] - 1u) << 31), make_double2(0.0, 0.0));
 }
 
@@ -1022,7 +1026,7 @@ void launch_gs_push(const RoundArgs& a, const Launch& l) {
 
 static unsigned scatter_blocks(const RoundArgs& a) {
     const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
-    return n > a.lo ? (n - a.lo + kScatterPer * kBlock - 1) / (kScatterPer * kBlock) : 0u;
+    return n > a.lo ? (n - a.lo + kShardPer * kBlock - 1) / (kShardPer * kBlock) : 0u;
 }
 
 void launch_ps_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l) {
