@@ -537,44 +537,51 @@ __global__ __launch_bounds__(kBlock) void k_shard_halo(RoundArgs a, Xchg x, int 
     }
 }
 
-// Round `applied`'s count into every send header; the entry counters restart at 0.  One wave:
-// lane s < kSub handles sub-segment s of every peer.
-__global__ void k_shard_pack(RoundArgs a, Xchg x, long long applied) {
-    unsigned long long newly = 0;
-    if (applied >= 0) newly = *part_slot(a.parts, applied, threadIdx.x);
+// Round `applied`'s count into every send header; the entry counters restart at 0.  One block
+// of kMaxWorld x kSub threads: thread (q, s) handles sub-segment s of peer q, all at once.
+static_assert(kMaxWorld * kSub == kBlock, "k_shard_pack maps one thread per (peer, sub-segment)");
+
+__global__ __launch_bounds__(kBlock) void k_shard_pack(RoundArgs a, Xchg x, long long applied) {
+    __shared__ unsigned long long newly_s;
+    __shared__ uint32_t of_s[kMaxWorld];
+    if (threadIdx.x < 64) {
+        unsigned long long newly = 0;
+        if (applied >= 0) newly = *part_slot(a.parts, applied, threadIdx.x);
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) newly += __shfl_xor(newly, off, 64);
-    if (threadIdx.x == 0) *x.self_newly = newly;
-    const uint32_t s = threadIdx.x;
-    const bool lane = s < kSub;
-    const uint32_t local_of = *x.overflow;
-    for (uint32_t q = 0; q < x.world; ++q) {
-        if (q == x.rank) continue;
-        ShardHeader* hd = x.out[q].hdr;
-        bool of = false;
-        if (lane) {
-            uint32_t* lc = ctr_at(x, q, s);
-            const uint32_t c = *lc;
-            hd->nlinks[s] = c < x.out[q].cap ? c : x.out[q].cap;
-            of = c > x.out[q].cap;
-            *lc = 0u;
-            const int side = q + 1 == x.rank ? 0 : q == x.rank + 1 ? 1 : -1;
-            uint32_t nh = 0;
-            if (side >= 0) {
-                uint32_t* hc = ctr_at(x, x.world + side, s);
-                const uint32_t n = *hc;
-                nh = n < x.h.out_cap[side] ? n : x.h.out_cap[side];
-                of = of || n > x.h.out_cap[side];
-                *hc = 0u;
-            }
-            hd->nhalo[s] = nh;
-        }
-        const unsigned long long any = __ballot(of);
+        for (int off = 32; off > 0; off >>= 1) newly += __shfl_xor(newly, off, 64);
         if (threadIdx.x == 0) {
-            hd->newly = newly;
-            hd->overflow = (any || local_of) ? 1u : 0u;
-            hd->pad = 0u;
+            *x.self_newly = newly;
+            newly_s = newly;
         }
+    }
+    if (threadIdx.x < kMaxWorld) of_s[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t q = threadIdx.x / kSub, s = threadIdx.x % kSub;
+    const bool peer = q < x.world && q != x.rank;
+    ShardHeader* hd = peer ? x.out[q].hdr : nullptr;
+    if (peer) {
+        uint32_t* lc = ctr_at(x, q, s);
+        const uint32_t c = *lc;
+        hd->nlinks[s] = c < x.out[q].cap ? c : x.out[q].cap;
+        bool of = c > x.out[q].cap;
+        *lc = 0u;
+        const int side = q + 1 == x.rank ? 0 : q == x.rank + 1 ? 1 : -1;
+        uint32_t nh = 0;
+        if (side >= 0) {
+            uint32_t* hc = ctr_at(x, x.world + side, s);
+            const uint32_t n = *hc;
+            nh = n < x.h.out_cap[side] ? n : x.h.out_cap[side];
+            of = of || n > x.h.out_cap[side];
+            *hc = 0u;
+        }
+        hd->nhalo[s] = nh;
+        if (of) atomicOr(&of_s[q], 1u);
+    }
+    __syncthreads();
+    if (peer && s == 0) {
+        hd->newly = newly_s;
+        hd->overflow = (of_s[q] || *x.overflow) ? 1u : 0u;
+        hd->pad = 0u;
     }
 }
 
@@ -1050,7 +1057,7 @@ void launch_shard_halo(const RoundArgs& a, const Xchg& x, int pushsum, hipStream
 }
 
 void launch_shard_pack(const RoundArgs& a, const Xchg& x, long long applied, hipStream_t s) {
-    hipLaunchKernelGGL(k_shard_pack, dim3(1), dim3(64), 0, s, a, x, applied);
+    hipLaunchKernelGGL(k_shard_pack, dim3(1), dim3(kBlock), 0, s, a, x, applied);
 }
 
 void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, uint32_t max_entries, int gossip,
