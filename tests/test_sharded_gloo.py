@@ -1,5 +1,5 @@
 """Multi-rank path on CPU: the product's shard host loop (gossip_amd.sharded.run) and its
-torch.distributed transport, over gloo with world_size 2 and 3, driving the CPU oracle's shard
+torch.distributed transport, over gloo with world_size 2, 3 and 8, driving the CPU oracle's shard
 engine (oracle.OracleShard).  Each rank owns the node range gp_partition gives it (whole
 z-planes for Imp3D/3D); the job must reproduce the single-process oracle bit for bit —
 completion trace, convergence round and every actor's state."""
@@ -98,6 +98,13 @@ def test_sharded_matches_single_process(case, world):
             assert sums[1] == pytest.approx(ref.layout.participants, rel=1e-12)
             assert sums[0] == pytest.approx(rs.sum_s, rel=1e-12)
     ref.close()
+
+
+@pytest.mark.parametrize("case", [(1000, "Imp3D", "push-sum", 1, 4000), (1000, "full", "gossip", 1, 4000)],
+                         ids=lambda c: f"{c[2]}-{c[1]}-{c[0]}")
+def test_sharded_world8(case):
+    """The driver's rank count (8 processes over gloo): the same host loop and transport."""
+    test_sharded_matches_single_process(case, 8)
 
 
 def test_uneven_partition_gossip_full():
