@@ -171,3 +171,28 @@ def test_cli_report_and_trace(tmp_path):
     np.testing.assert_array_equal(rows[:, 1], cpu.read_trace())
     assert rows[-1, 1] == int(cpu.layout.nodes)
     cpu.close()
+
+def _sweep_cases(count=64, seed=2026):
+    """Seeded random (n, topology, algorithm, seed, generic) draws: sizes log-uniform over
+    2..200000, so grid sizes that are not cubes/squares and ragged last planes all appear."""
+    rng = np.random.default_rng(seed)
+    topos = sorted(oracle.TOPOLOGIES)
+    out = []
+    for _ in range(count):
+        n = int(np.exp(rng.uniform(np.log(2), np.log(200000))))
+        out.append((n, topos[rng.integers(len(topos))], ("gossip", "push-sum")[rng.integers(2)],
+                    int(rng.integers(1, 1 << 30)), bool(rng.integers(2))))
+    return out
+
+
+@pytest.mark.parametrize("n,topo,algo,seed,generic", _sweep_cases())
+def test_random_sweep(n, topo, algo, seed, generic):
+    """Bit-exact against the oracle over random configurations, to convergence or 2000 rounds."""
+    gpu = Simulator(n, topo, algo, seed=seed, generic=generic)
+    cpu = oracle.OracleSim(n, topo, algo, seed=seed)
+    gs = gpu.step(2000)
+    cs = cpu.step(2000, threads=8)
+    assert (gs.round, gs.completed, gs.converged) == (cs.round, cs.completed, cs.converged)
+    np.testing.assert_array_equal(gpu.read_trace(), cpu.read_trace())
+    check_same(gpu, cpu, algo)
+    gpu.close()
