@@ -151,3 +151,36 @@ def test_shard_errors():
     assert e.lib.gp_read_pushsum(e.h, e.hi, 1, p, p, None) == -1  # another rank's actor
     assert e.lib.gp_step(e.h, 1, None) == -4  # a shard advances with gp_shard_round
     e.close()
+
+
+def _sweep_cases(count=40, seed=7):
+    """Seeded random (n, topology, algorithm, seed, world) draws for the shard engine: sizes
+    log-uniform over 64..200000, 2..8 ranks (push-sum on "full" is single-GPU only)."""
+    rng = np.random.default_rng(seed)
+    topos = sorted(oracle.TOPOLOGIES)
+    out = []
+    while len(out) < count:
+        n = int(np.exp(rng.uniform(np.log(64), np.log(200000))))
+        topo, algo = topos[rng.integers(len(topos))], ("gossip", "push-sum")[rng.integers(2)]
+        case = (n, topo, algo, int(rng.integers(1, 1 << 30)), int(rng.integers(2, 9)))
+        if not (topo == "full" and algo == "push-sum"):
+            out.append(case)
+    return out
+
+
+@pytest.mark.parametrize("n,topo,algo,seed,world", _sweep_cases())
+def test_shards_random_sweep(n, topo, algo, seed, world):
+    """Loopback shards bit-exact against the oracle over random configurations (2000 rounds max)."""
+    try:
+        sharded.partition(n, topo, world)
+    except GossipError:
+        pytest.skip("graph has fewer z-planes than ranks")
+    ref = oracle.OracleSim(n, topo, algo, seed=seed)
+    engines = _shards(n, topo, algo, world, seed)
+    rs = ref.step(2000, threads=8)
+    sts = sharded.run_local(engines, max_rounds=int(rs.round))
+    for st in sts:
+        assert (st.round, st.completed, st.converged) == (rs.round, rs.completed, rs.converged)
+    _check_vs(ref, engines, algo)
+    for e in engines:
+        e.close()
