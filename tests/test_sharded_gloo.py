@@ -139,3 +139,32 @@ def test_partition_rules():
         sharded.partition(20, "Imp3D", 8)  # 2 z-planes cannot feed 8 ranks
     with pytest.raises(GossipError):
         sharded.partition(1000, "Imp3D", 17)  # more ranks than the exchange supports
+
+
+def _sweep_cases(count=8, seed=12):
+    """Seeded random (n, topology, algorithm, seed) draws over 2..5 ranks (no push-sum on
+    "full": single-GPU only); sizes log-uniform over 64..3000."""
+    rng = np.random.default_rng(seed)
+    topos = ["2D", "3D", "Imp3D", "full", "line"]
+    out = []
+    while len(out) < count:
+        n = int(np.exp(rng.uniform(np.log(64), np.log(3000))))
+        topo, algo = topos[rng.integers(len(topos))], ("gossip", "push-sum")[rng.integers(2)]
+        world = int(rng.integers(2, 6))
+        if topo == "full" and algo == "push-sum":
+            continue
+        out.append(((n, topo, algo, int(rng.integers(1, 1 << 30)), 3000), world))
+    return out
+
+
+@pytest.mark.parametrize("case,world", _sweep_cases(), ids=lambda c: str(c))
+def test_sharded_random_sweep(case, world):
+    """Random configurations through the product host loop and gloo transport, bit-exact
+    against one process."""
+    from gossip_amd import GossipError, sharded
+
+    try:
+        sharded.partition(case[0], case[1], world)
+    except GossipError:
+        pytest.skip("graph has fewer z-planes than ranks")
+    test_sharded_matches_single_process(case, world)
