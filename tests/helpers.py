@@ -1,6 +1,9 @@
 """Shared comparison helpers for oracle / golden / HIP parity tests."""
+import base64
+import hashlib
 import json
 import os
+import zlib
 
 import numpy as np
 
@@ -36,6 +39,61 @@ def check_state(sim, g, prefix):
         np.testing.assert_array_equal(d, g[prefix + "msg_dst"])
         np.testing.assert_array_equal(bits(s), bits(g[prefix + "msg_s"]))
         np.testing.assert_array_equal(bits(w), bits(g[prefix + "msg_w"]))
+
+
+DIGEST_CHUNKS = 16
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def digest_arrays(arrays):
+    """{name: {"all": sha256, "chunks": [16 x sha256]}} of full-range state arrays (little
+    endian; fp64 compared as bits)."""
+    out = {}
+    for k, a in arrays.items():
+        if a.dtype == np.float64:
+            a = a.view(np.uint64)
+        out[k] = {"all": _sha(a), "chunks": [_sha(c) for c in np.array_split(a, DIGEST_CHUNKS)]}
+    return out
+
+
+def state_arrays(sim, algo):
+    """Full-range state of any engine with the read_* API (oracle.OracleSim, gossip_amd.Simulator)."""
+    if algo in (0, "gossip"):
+        cnt, flags = sim.read_gossip()
+        return {"cnt": cnt, "flags": flags}
+    S, W, flags = sim.read_pushsum()
+    d, s, w = sim.read_messages()
+    return {"S": S, "W": W, "flags": flags, "msg_dst": d, "msg_s": s, "msg_w": w}
+
+
+def state_digests(sim, algo):
+    return digest_arrays(state_arrays(sim, algo))
+
+
+def compare_digests(got, want):
+    """Assert two digest dicts are equal; on a mismatch name the array and the first chunk."""
+    assert set(got) == set(want), (sorted(got), sorted(want))
+    for k in want:
+        if got[k]["all"] != want[k]["all"]:
+            bad = [i for i, (a, b) in enumerate(zip(got[k]["chunks"], want[k]["chunks"])) if a != b]
+            raise AssertionError(f"state array {k!r} differs from the oracle fingerprint in chunks {bad} "
+                                 f"(of {DIGEST_CHUNKS})")
+
+
+def pack_trace(trace):
+    return base64.b64encode(zlib.compress(np.asarray(trace, np.int64).tobytes(), 9)).decode()
+
+
+def unpack_trace(z):
+    return np.frombuffer(zlib.decompress(base64.b64decode(z)), np.int64)
+
+
+def fingerprints():
+    with open(os.path.join(GOLD, "fingerprints.json")) as f:
+        return json.load(f)
 
 
 def check_same(a, b, algo):

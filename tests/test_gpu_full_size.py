@@ -1,13 +1,12 @@
-"""BASELINE configs 4 and 5 at their full sizes on one GPU, checked through size-independent
-properties (the CPU oracle cannot run them in test time; parity at these sizes rests on the
-bit-exact tests at <= 10M and on these invariants).
+"""BASELINE config 5 at its full size on one GPU, checked through size-independent properties:
+the CPU oracle cannot hold a 1e9-node run in the build container, so parity at this size rests
+on the bit-exact fingerprint tests up to 1e8 nodes (test_gpu_fingerprints.py: C3 10M to
+convergence, C4 100M full gossip to convergence, a 50-round window of 100M Imp3D push-sum) and
+on these invariants.
 
   config 5: `1000000000 Imp3D push-sum` (1e9 nodes, G = 1148, 759 planes): a fixed 12-round
             window — sum(S) and sum(W) over held + in-flight messages conserved (program.fs:107-143
             only moves mass), the completion trace monotone, every estimate finite.
-  config 4: `100000000 full gossip` to convergence: all `nodes` reports counted (program.fs:49),
-            every reported actor received more than 10 rumours (program.fs:102), the trace
-            monotone and ending exactly at the convergence round.
 """
 import numpy as np
 import pytest
@@ -33,19 +32,4 @@ def test_imp3d_1e9_pushsum_window():
     for first in (0, 500_000_000, sim.nodes - 1_000_000):
         S, W, _ = sim.read_pushsum(first, 1_000_000)
         assert np.isfinite(S).all() and (W > 0).all()
-    sim.close()
-
-
-def test_full_gossip_1e8_converges():
-    sim = Simulator(100_000_000, "full", "gossip", seed=1)
-    assert sim.nodes == 100_000_000 and sim.actors == 100_000_001
-    st = sim.step()
-    assert st.converged and st.completed >= sim.nodes
-    tr = sim.read_trace()
-    assert len(tr) == st.round and (np.diff(tr) >= 0).all()
-    assert tr[-1] >= sim.nodes and (len(tr) == 1 or tr[-2] < sim.nodes)
-    cnt, flags = sim.read_gossip()
-    done = (flags & 4) != 0
-    assert int(done.sum()) == int(tr[-1])
-    assert (cnt[done] > 10).all()
     sim.close()

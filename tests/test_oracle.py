@@ -121,3 +121,18 @@ def test_gossip_invariants():
         # done nodes are frozen
         assert (cnt[prev_done] == prev_cnt[prev_done]).all()
         prev_cnt, prev_done = cnt, done
+
+
+def test_fingerprint_fixture_reproduces():
+    """The full-size fixture (tests/golden/fingerprints.json) is what the oracle computes: its
+    smallest case re-run here, single-thread canonical order, matches trace and every digest."""
+    from helpers import compare_digests, fingerprints, state_digests, unpack_trace
+
+    fp = fingerprints()["C2_line_100k_pushsum"]
+    sim = oracle.OracleSim(fp["n_arg"], fp["topology"], fp["algorithm"], seed=fp["seed"])
+    st = sim.step(fp["cap"])
+    assert (st.round, st.completed, st.converged) == (fp["rounds"], fp["completed"], fp["converged"])
+    np.testing.assert_array_equal(sim.read_trace(), unpack_trace(fp["trace_z"]))
+    compare_digests(state_digests(sim, fp["algorithm"]), fp["digests"])
+    assert st.sum_s == float.fromhex(fp["sum_s"]) and st.sum_w == float.fromhex(fp["sum_w"])
+    sim.close()

@@ -1,0 +1,46 @@
+# One launcher for GPU-box runs (gpurun -- 'bash tools/gpu.sh MODE').  Everything lands in
+# gpurun_out/<MODE>/; every GPU step has its own time limit and the script stops at the first
+# failing step.
+#   tests   pytest -m gpu
+#   iter    tests + a bench line (no CPU baseline) + a kernel trace of 300 rounds (prof_run.py)
+#   bench   the default bench.py line (with the CPU baseline) + its rocprofv3 kernel trace/stats
+#   pmc     FETCH_SIZE and WRITE_SIZE passes (one run each) over 60 rounds of prof_run.py
+#   ab      kernel-trace A/B of the variant libraries named in $VARIANTS (lib_<name>/, GP_LIB)
+# Extra prof_run.py arguments: $PROF_ARGS; rounds: $ROUNDS.
+set -o pipefail
+R="$GRAFT_REPO_ROOT"; cd "$R"
+MODE=${1:-iter}
+O="$R/gpurun_out/$MODE"; rm -rf "$O"; mkdir -p "$O"
+step() { echo "== $*"; }
+tests() {
+  timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TEST_ARGS} > "$O/gpu_tests.log" 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -4 "$O/gpu_tests.log"; return $rc
+}
+kt() {  # $1 = output name, rest = command
+  local n=$1; shift
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 ${KT_TIMEOUT:-240} rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$n" -o kt -- "$@" > "$O/$n.log" 2>&1 )
+  rc=$?; echo "kt $n rc=$rc"; tail -1 "$O/$n.log"; [ $rc -eq 0 ] || return $rc
+  python3 "$R/tools/kt_summary.py" "$O/$n/kt_kernel_trace.csv" | head -${KT_LINES:-6}
+}
+case $MODE in
+  tests) tests ;;
+  iter)
+    tests || exit $?
+    timeout -k 10 240 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > "$O/bench.json" 2> "$O/bench.err"
+    rc=$?; echo "bench rc=$rc"; cat "$O/bench.json"; [ $rc -eq 0 ] || exit $rc
+    kt kt python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-300} ${PROF_ARGS} ;;
+  bench)
+    timeout -k 10 300 python3 bench.py ${BENCH_ARGS} > "$O/bench.json" 2> "$O/bench.err"
+    rc=$?; echo "bench rc=$rc"; cat "$O/bench.json"; [ $rc -eq 0 ] || exit $rc
+    kt kt python3 "$R/bench.py" --no-cpu-baseline ${BENCH_ARGS} ;;
+  pmc)
+    for c in FETCH_SIZE WRITE_SIZE ${PMC_EXTRA}; do
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_$c" -o p -- python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-60} ${PROF_ARGS} > "$O/pmc_$c.log" 2>&1 )
+      rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+    done ;;
+  ab)
+    for v in ${VARIANTS}; do
+      GP_LIB=lib_$v kt "kt_$v" python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-300} ${PROF_ARGS} || exit $?
+    done ;;
+  *) echo "unknown mode $MODE"; exit 2 ;;
+esac
