@@ -1,13 +1,21 @@
 // gossip_cli.cpp — drop-in replacement for the reference's program entry point.
 //
-//   gossip numNodes topology algorithm [--seed S] [--max-rounds R] [--device D] [--quiet]
-//          [--trace FILE]
+//   gossip numNodes topology algorithm [--seed S] [--max-rounds R] [--device D] [--gpus N]
+//          [--mode round] [--verbose] [--trace FILE]
 //
 // Same positional contract as /root/reference/program.fs:19-21 (argv[1] = numNodes,
 // argv[2] = topology "line" | "full" | "2D" | "Imp3D" (+ build-defined "3D"), argv[3] =
 // algorithm "gossip" | "push-sum"), the same banners (program.fs:180,186,217,222,257,262,
 // 322,327) and the same final report (program.fs:51-52 / 58-59).  The Akka actor system is
-// replaced by libgossip_hip.so; a "Rounds:" line is added after the report.
+// replaced by libgossip_hip.so.  stdout is exactly the reference's lines — the banner, the
+// separator, `Convergence Time: %f ms` — plus one `Rounds: N` line; --verbose adds the layout
+// (actors, nodes, leader) after the banner.
+//
+// --gpus N runs the one graph over N GPUs of this process (gp_config.num_gpus: node-range
+// shards, RCCL exchange inside the library).  --mode round is the synchronous-round engine (the
+// only mode); the reference's asynchronous actor execution is not part of the engine: its
+// statistical restatement is test infrastructure (oracle/gp_async.c), so --mode async is
+// refused.
 //
 // Deliberate deviations: an invalid algorithm or topology exits with status 2
 // instead of hanging at Console.ReadLine() (program.fs:188-189, 331-334); a run that hits
@@ -44,7 +52,9 @@ const char* banner(int topo, int algo) {
 
 int main(int argc, char** argv) {
     if (argc < 4) {
-        std::fprintf(stderr, "usage: %s numNodes topology algorithm [--seed S] [--max-rounds R] [--device D] [--quiet] [--trace FILE]\n",
+        std::fprintf(stderr,
+                     "usage: %s numNodes topology algorithm [--seed S] [--max-rounds R] [--device D] [--gpus N] "
+                     "[--mode round] [--verbose] [--trace FILE]\n",
                      argv[0]);
         return 2;
     }
@@ -57,16 +67,25 @@ int main(int argc, char** argv) {
     cfg.term_init = 1;
     cfg.term_limit = 3;
     long long max_rounds = 1LL << 40;
-    bool quiet = false;
+    bool verbose = false;
     const char* trace_path = nullptr;
     for (int i = 4; i < argc; ++i) {
         const std::string a = argv[i];
         if (a == "--seed" && i + 1 < argc) cfg.seed = std::strtoull(argv[++i], nullptr, 10);
         else if (a == "--max-rounds" && i + 1 < argc) max_rounds = std::strtoll(argv[++i], nullptr, 10);
         else if (a == "--device" && i + 1 < argc) cfg.device = std::atoi(argv[++i]);
-        else if (a == "--quiet") quiet = true;
+        else if (a == "--gpus" && i + 1 < argc) cfg.num_gpus = std::atoi(argv[++i]);
+        else if (a == "--verbose") verbose = true;
         else if (a == "--trace" && i + 1 < argc) trace_path = argv[++i];
-        else {
+        else if (a == "--mode" && i + 1 < argc) {
+            const std::string m = argv[++i];
+            if (m != "round") {
+                std::fprintf(stderr, "--mode %s: only the synchronous-round engine (--mode round) is built; the "
+                                     "asynchronous actor model is a CPU test model (oracle/gp_async.c)\n",
+                             m.c_str());
+                return 2;
+            }
+        } else {
             std::fprintf(stderr, "unknown option %s\n", a.c_str());
             return 2;
         }
@@ -91,9 +110,9 @@ int main(int argc, char** argv) {
         return 1;
     }
     std::printf("%s\n", banner(topo, cfg.algo));
-    if (!quiet)
-        std::printf("actors %lld (nodes %lld), leader %lld\n", (long long)lay.actors, (long long)lay.nodes,
-                    (long long)lay.leader);
+    if (verbose)
+        std::printf("actors %lld (nodes %lld), leader %lld, %d GPU(s)\n", (long long)lay.actors, (long long)lay.nodes,
+                    (long long)lay.leader, cfg.num_gpus > 1 ? cfg.num_gpus : 1);
     gp_status st{};
     if (gp_step(h, max_rounds, &st) != GP_OK) {
         std::fprintf(stderr, "gp_step: %s\n", gp_last_error());

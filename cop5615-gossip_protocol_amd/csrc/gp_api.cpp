@@ -4,8 +4,10 @@
 // the round loop that replaces the actor dispatch (program.fs:82-146) and the ParentActor
 // count (program.fs:44-63), and state read-back.  All per-actor work runs in gp_kernels.hip.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -80,7 +82,10 @@ struct Chunk {
 constexpr size_t kAlign = 256;
 size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
+struct Group;
+
 struct Handle {
+    Group* grp = nullptr;  // num_gpus > 1: this handle is the whole graph over the group's shards
     gp_config cfg{};
     gp_layout lay{};
     Geom g{};
@@ -108,7 +113,6 @@ struct Handle {
     std::vector<void*> allocs;
     size_t dev_bytes = 0;
     // topology
-    uint32_t* link = nullptr;
     uint32_t* rev_off = nullptr;
     uint32_t* rev_src = nullptr;
     uint32_t* lpos = nullptr;
@@ -142,7 +146,6 @@ struct Handle {
     int64_t completed = 0;
     bool converged = false;
     int64_t batch = 8;
-    uint32_t ablate = 0;  // DEBUG: GP_ABLATE env var (cost attribution only; breaks results)
     // timing
     std::vector<hipEvent_t> kev;  // 3 per round: before main, after main, after aux
     hipEvent_t ev_a = nullptr, ev_b = nullptr;
@@ -162,16 +165,23 @@ struct Handle {
     }
 
     // Device array holding elements [first, first + count) of a global index space; *p is
-    // biased by -first so kernels index it with global actor / slot ids.
+    // biased by -first so kernels index it with global actor / slot ids.  The element range is
+    // widened to start at a multiple of 16 (so the tile kernel's whole-dword / 16-byte loads of
+    // actors v0 .. v0+3, v0 a multiple of 4, are aligned where they must be) and padded by 256
+    // bytes on both sides: the row loads of the first and last lanes (v0 - 2 .. v0 + 5, a lane's
+    // 16 link marks) read a few elements past [first, first + count) and never use them.
     template <class T>
     int alloc(T** p, size_t count, int64_t first = 0) {
+        constexpr size_t kPad = 256;
+        const int64_t f0 = first & ~(int64_t)15;
+        const size_t n = (size_t)(first - f0) + count;
         void* q = nullptr;
-        const size_t bytes = count * sizeof(T) + 64;  // padding: vectorised tail reads stay in bounds
+        const size_t bytes = n * sizeof(T) + 2 * kPad;
         hipError_t e = hipMalloc(&q, bytes);
         if (e != hipSuccess) return fail(GP_ENOMEM, "hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
         allocs.push_back(q);
         dev_bytes += bytes;
-        *p = reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(q) - (uintptr_t)first * sizeof(T));
+        *p = reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(q) + kPad - (uintptr_t)f0 * sizeof(T));
         return GP_OK;
     }
 
@@ -188,6 +198,11 @@ struct Handle {
         a.seed = cfg.seed;
         a.lo = lo;
         a.hi = hi;
+        a.tile0 = lo & ~(kTileK - 1u);
+        a.ntiles = (hi - a.tile0 + kTileActors - 1u) / kTileActors;
+        a.tag_prev = r ? link_tag(r - 1u) : 0u;
+        a.tag_cur = link_tag(r);
+        a.ps_tags = gossip ? 0u : 1u;
         a.slot_lo = sbnd.empty() ? 0u : (uint32_t)sbnd[rank];
         a.sharded = sharded ? 1u : 0u;
         a.r = r;
@@ -198,10 +213,8 @@ struct Handle {
         a.threshold = (uint32_t)cfg.gossip_threshold;
         a.delta = cfg.delta;
         a.term_limit = (uint32_t)cfg.term_limit;
-        a.ablate = ablate;
         a.total = total;
         a.parts = parts;
-        a.link = link;
         a.rev_off = rev_off;
         a.rev_src = rev_src;
         a.lpos = lpos;
@@ -234,68 +247,101 @@ Handle* H(void* h) { return static_cast<Handle*>(h); }
 
 Xchg base_xchg(const Handle* h);
 
-// Imp3D extra links (program.fs:309) and their receiver-side CSR, for the whole graph: each
-// rank draws every link itself (Philox is global), so no exchange is needed to learn which
-// remote senders target its actors or at which CSR slot.  A shard keeps link slots for its
-// own destinations only.
+// Imp3D extra links (program.fs:309) and their receiver-side CSR.  A rank keeps only its own
+// slices: rev_off / rev_src for the destinations it owns ([lo, hi) and their CSR slots
+// [slo, shi)), lpos for the senders it owns.  No rank stores the link array: link_of() recomputes
+// a link from (seed, sender), so every rank knows every link without an exchange — which remote
+// senders target its actors, at which global slot, and the per-peer link counts that size the
+// exchange.  Three transient arrays over all destinations (counts, offsets, the own senders'
+// offsets) live only during the build.
 int build_links(Handle* h) {
     const uint32_t nodes = (uint32_t)h->lay.nodes, A = h->g.actors;
+    const uint32_t lo = h->lo, hi = h->hi, shi_src = std::min(hi, nodes);  // own senders [lo, shi_src)
+    const uint64_t seed = h->cfg.seed;
     int rc;
-    if ((rc = h->alloc(&h->link, nodes))) return rc;
-    if ((rc = h->alloc(&h->rev_off, (size_t)A + 1))) return rc;
-    if ((rc = h->alloc(&h->rev_src, nodes))) return rc;
-    if (!h->generic && (rc = h->alloc(&h->lpos, nodes))) return rc;
-    uint32_t *counts = nullptr, *scratch = nullptr;
-    HIP_TRY(hipMalloc(&counts, ((size_t)A + 1) * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc(&scratch, scan_scratch_words(A) * sizeof(uint32_t)));
+    if ((rc = h->alloc(&h->rev_off, (size_t)(hi - lo) + 1, lo))) return rc;
+    if (!h->generic && shi_src > lo && (rc = h->alloc(&h->lpos, (size_t)(shi_src - lo), lo))) return rc;
+    const size_t nA = (size_t)A + 1;
+    uint32_t *X = nullptr, *Y = nullptr, *Z = nullptr, *list = nullptr, *scratch = nullptr;
+    auto cleanup = [&]() {
+        for (uint32_t* p : {X, Y, Z, list, scratch})
+            if (p) (void)hipFree(p);
+    };
+    if (hipMalloc(&X, nA * 4) != hipSuccess || hipMalloc(&Y, nA * 4) != hipSuccess || hipMalloc(&Z, nA * 4) != hipSuccess ||
+        hipMalloc(&list, ((size_t)(shi_src > lo ? shi_src - lo : 0) + 1) * 4) != hipSuccess ||
+        hipMalloc(&scratch, scan_scratch_words(A + 1) * 4) != hipSuccess) {
+        cleanup();
+        return fail(GP_ENOMEM, "extra-link CSR build: transient arrays of %zu bytes", 3 * nA * 4);
+    }
     const Launch l = h->L();
+    hipStream_t s = h->stream;
     hipError_t e = hipSuccess;
-    launch_links(h->link, nodes, h->cfg.seed, l);
-    e = hipMemsetAsync(counts, 0, ((size_t)A + 1) * sizeof(uint32_t), h->stream);
+    std::vector<uint32_t> sb((size_t)h->world + 1);
+    // X = links per destination (all senders); Y = their exclusive scan = global CSR offsets
+    e = hipMemsetAsync(X, 0, nA * 4, s);
     if (e == hipSuccess) {
-        launch_count(h->link, nodes, counts, l);
-        launch_exclusive_scan(counts, h->rev_off, A, scratch, h->stream);
-        e = hipMemsetAsync(counts, 0, ((size_t)A + 1) * sizeof(uint32_t), h->stream);
+        launch_dst_count(seed, nodes, 0, nodes, X, l);
+        launch_exclusive_scan(X, Y, A + 1, scratch, s);
+        e = hipMemcpyAsync(h->rev_off + lo, Y + lo, (size_t)(hi - lo + 1) * 4, hipMemcpyDeviceToDevice, s);
     }
+    for (int q = 0; q <= h->world && e == hipSuccess; ++q)  // link-slot bounds of every rank
+        e = hipMemcpyAsync(&sb[(size_t)q], Y + h->abnd[q], 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    const uint32_t slo = sb[(size_t)h->rank], shi = sb[(size_t)h->rank + 1];
+    if (e == hipSuccess && (rc = h->alloc(&h->rev_src, (size_t)(shi - slo), slo))) {
+        cleanup();
+        return rc;
+    }
+    // own destinations' sources, ascending per destination
+    if (e == hipSuccess) e = hipMemsetAsync(X, 0, nA * 4, s);
     if (e == hipSuccess) {
-        launch_rev_fill(h->link, nodes, h->rev_off, counts, h->rev_src, l);
-        launch_sort_segments(h->rev_off, h->rev_src, A, l);  // ascending sources per destination
-        if (h->lpos) launch_lpos(h->rev_src, nodes, h->lpos, l);
-        e = hipStreamSynchronize(h->stream);
+        launch_dst_fill(seed, nodes, 0, nodes, lo, hi, Y, X, h->rev_src, l);
+        launch_sort_segments(h->rev_off + lo, h->rev_src, hi - lo, l);
     }
+    // lpos of the own senders: base[t] = Y[t] + links into t from senders below lo; the own
+    // senders' per-destination lists (Z-offsets, sorted) give each one's place after that
+    if (e == hipSuccess && !h->generic && shi_src > lo) {
+        e = hipMemsetAsync(X, 0, nA * 4, s);
+        if (e == hipSuccess) e = hipMemsetAsync(Z, 0, nA * 4, s);
+        if (e == hipSuccess) {
+            launch_dst_count(seed, nodes, 0, lo, X, l);
+            launch_add_u32(X, Y, A + 1, l);
+            launch_dst_count(seed, nodes, lo, shi_src, Z, l);
+            launch_exclusive_scan(Z, Y, A + 1, scratch, s);
+            e = hipMemsetAsync(Z, 0, nA * 4, s);
+        }
+        if (e == hipSuccess) {
+            launch_dst_fill(seed, nodes, lo, shi_src, 0, A, Y, Z, list, l);
+            launch_sort_segments(Y, list, A, l);
+            launch_lpos_lists(Y, list, A, X, h->lpos, l);
+        }
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e == hipSuccess) e = hipGetLastError();
-    (void)hipFree(counts);
-    (void)hipFree(scratch);
+    cleanup();
     if (e != hipSuccess) return fail(GP_EHIP, "extra-link CSR build failed: %s", hipGetErrorString(e));
     h->lay.links = nodes;
-    // link-slot range of every rank (contiguous: destinations are)
-    h->sbnd.assign((size_t)h->world + 1, 0);
-    for (int q = 0; q <= h->world; ++q) {
-        uint32_t v = 0;
-        HIP_TRY(hipMemcpy(&v, h->rev_off + h->abnd[q], sizeof v, hipMemcpyDeviceToHost));
-        h->sbnd[q] = v;
-    }
-    const int64_t slo = h->sbnd[h->rank], nsl = h->sbnd[h->rank + 1] - slo;
+    h->sbnd.assign(sb.begin(), sb.end());
+    const int64_t nsl = (int64_t)shi - slo;
     if (!h->generic) {  // pull kernels
-        // per-slot link counts of local senders (gossip chains, push-sum messages)
+        // per-slot link marks of the own slots (gossip chains, push-sum round tags)
         if ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))) return rc;
-        // a remote sender's link message lands in the receiver's slot, read in CSR order (k_ps_pull<2>)
+        // a remote sender's link message lands in the receiver's slot, read in CSR order (k_ps_tile<2>)
         if (h->sharded && h->world > 1 && !h->gossip &&
             ((rc = h->alloc(&h->rmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->rmsg[1], (size_t)nsl, slo))))
             return rc;
-
     }
     if (h->sharded) {  // link counts per (source rank, destination rank, sender degree)
         const size_t nb = (size_t)h->world * h->world * 8;
         unsigned long long* hist = nullptr;
         HIP_TRY(hipMalloc(&hist, nb * sizeof *hist));
-        e = hipMemsetAsync(hist, 0, nb * sizeof *hist, h->stream);
+        e = hipMemsetAsync(hist, 0, nb * sizeof *hist, s);
         if (e == hipSuccess) {
-            launch_link_hist(h->link, h->g, base_xchg(h), hist, l);
+            launch_link_hist(seed, h->g, base_xchg(h), hist, l);
             h->lhist.assign(nb, 0);
-            e = hipMemcpyAsync(h->lhist.data(), hist, nb * sizeof *hist, hipMemcpyDeviceToHost, h->stream);
+            e = hipMemcpyAsync(h->lhist.data(), hist, nb * sizeof *hist, hipMemcpyDeviceToHost, s);
         }
-        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
         (void)hipFree(hist);
         if (e != hipSuccess) return fail(GP_EHIP, "link histogram failed: %s", hipGetErrorString(e));
     }
@@ -388,7 +434,7 @@ int reset(Handle* h) {
 const char* round_kernel_name(const Handle* h) {
     if (h->gossip) return h->generic ? "k_gs_push" : (h->g.has_link ? "k_gs_pull<true>" : "k_gs_pull<false>");
     if (h->generic) return "k_ps_push_emit";
-    return h->g.has_link ? (h->rmsg[0] ? "k_ps_pull<2>" : "k_ps_pull<1>") : "k_ps_pull<0>";
+    return h->g.has_link ? (h->rmsg[0] ? "k_ps_tile<2>" : "k_ps_tile<1>") : "k_ps_tile<0>";
 }
 
 const char* aux_kernel_name(const Handle* h) {
@@ -434,15 +480,19 @@ void launch_main(Handle* h, int64_t k, const Xchg* x) {
     } else if (h->generic) {
         launch_ps_push_emit(a, l);
     } else {
-        launch_ps_pull(a, l);
+        launch_ps_tile(a, l);
     }
 }
 
 // ... and the passes that complete round k after it (link scatter; bucket scan + fill).
-void launch_aux(Handle* h, int64_t k, const Xchg* x) {
+int launch_aux(Handle* h, int64_t k, const Xchg* x) {
     const uint32_t r = (uint32_t)k;
     const RoundArgs a = h->args(r);
     const Launch l = h->L();
+    if (!h->gossip && h->lcnt[0] && tag_clear_round(r)) {  // this parity's tags are about to repeat
+        const int64_t slo = h->sbnd[h->rank], ns = h->sbnd[h->rank + 1] - slo;
+        HIP_TRY(hipMemsetAsync(h->lcnt[r & 1u] + slo, 0, (size_t)ns, h->stream));
+    }
     if (h->gossip) {
         if (!h->generic && h->g.has_link) {
             if (x) launch_gs_link_scatter_x(a, *x, l);
@@ -456,6 +506,7 @@ void launch_aux(Handle* h, int64_t k, const Xchg* x) {
         if (x) launch_ps_link_scatter_x(a, *x, l);
         else launch_link_count(a, l);
     }
+    return GP_OK;
 }
 
 constexpr int64_t kTimeEvery = 8;  // kernel timing: one round in 8
@@ -474,7 +525,8 @@ int launch_round(Handle* h, int64_t k, const Xchg* x, bool timing, int64_t i) {
     if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i], h->stream));
     launch_main(h, k, x);
     if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i + 1], h->stream));
-    launch_aux(h, k, x);
+    int rc;
+    if ((rc = launch_aux(h, k, x))) return rc;
     if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i + 2], h->stream));
     return GP_OK;
 }
@@ -924,17 +976,13 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
     if (h->world > 1 && !h->full) h->halo = g.gz > 1 ? g.plane : 1u;  // grid rows crossing a shard face
     // leader = Random().Next(0, nodes)  (program.fs:173/211/250/316)
     h->lay.leader = scale_draw(philox(0u, 0u, kStreamLeader, cfg->seed).x, (uint32_t)nodes);
-    int64_t part = 0;
-    if (h->full) part = actors;
-    else
-        for (int64_t v = 0; v < actors; ++v) part += presence(g, (uint32_t)v) != 0u;
-    h->lay.participants = part;
-    if (const char* ab = std::getenv("GP_ABLATE")) h->ablate = (uint32_t)std::strtoul(ab, nullptr, 0);
+    // actors with at least one neighbour: every actor of line / 2D / full (nodes + 1 >= 2),
+    // every wired node of Imp3D (its extra link, program.fs:309), every node of a 3D grid of
+    // more than one node (the only grid without edges is the single node, N < 8)
+    if (cfg->topology == GP_IMP3D) h->lay.participants = nodes;
+    else if (cfg->topology == GP_THREE_D) h->lay.participants = nodes > 1 ? nodes : 0;
+    else h->lay.participants = actors;
     h->grid = grid_for(h->own());
-    if (const char* gg = std::getenv("GP_GRID")) {  // tuning override (rounded to a multiple of 8)
-        const long v = std::strtol(gg, nullptr, 0);
-        if (v >= 8) h->grid = (int)((v + 7) / 8 * 8);
-    }
     h->span = span_for(h->own(), h->grid);
 
     auto bail = [&](int code) {
@@ -999,6 +1047,233 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
     return GP_OK;
 }
 
+// ------------------------------------------------------------------ single-process multi-GPU
+// gp_create with cfg->num_gpus = N > 1 ("the library owns ... RCCL comms; multi-GPU
+// runs inside one process, one stream per device, ncclCommInitAll plus group calls").  The graph
+// is split into N node-range shards (gp_partition), shard p on device device + p with its own
+// stream; a round is every shard's gp_shard_round, ONE exchange of the fixed-size chunks, every
+// shard's gp_shard_deliver — the same decomposition the torch.distributed host drives over one
+// process per GPU (gossip_amd/sharded.py), here with the library's own transport:
+//   * RCCL: one communicator per device from ncclCommInitAll; the exchange is one
+//     ncclGroupStart / ncclGroupEnd around every (p, q) ncclSend / ncclRecv pair, each on the
+//     sending / receiving shard's stream, so kernels and transfers stay stream-ordered;
+//   * GP_FLAG_ONE_DEVICE (tests on one GPU): every shard on cfg->device, one shared stream,
+//     the chunks moved by device copies.
+struct Group {
+    int W = 0;
+    bool one_device = false;
+    std::vector<Handle*> shard;
+    std::vector<int> dev;
+    std::vector<void*> send, recv;
+    std::vector<ncclComm_t> comm;
+    hipStream_t shared = nullptr;
+    int64_t batch = 8;
+    int64_t rounds = 0, completed = 0;
+    bool converged = false;
+
+    ~Group() {
+        for (size_t p = 0; p < shard.size(); ++p) {
+            if (!one_device) (void)hipSetDevice(dev[p]);
+            if (shard[p]) (void)hipStreamSynchronize(shard[p]->stream);
+        }
+        for (ncclComm_t c : comm)
+            if (c) (void)ncclCommDestroy(c);
+        for (size_t p = 0; p < shard.size(); ++p) {
+            if (!one_device) (void)hipSetDevice(dev[p]);
+            if (p < send.size() && send[p]) (void)hipFree(send[p]);
+            if (p < recv.size() && recv[p]) (void)hipFree(recv[p]);
+            delete shard[p];
+        }
+        if (shared) (void)hipStreamDestroy(shared);
+    }
+};
+
+#define RCCL_TRY(x)                                                                                \
+    do {                                                                                           \
+        ncclResult_t r_ = (x);                                                                     \
+        if (r_ != ncclSuccess) return fail(GP_ERCCL, "%s failed: %s", #x, ncclGetErrorString(r_)); \
+    } while (0)
+
+int group_exchange(Group& G) {
+    const int W = G.W;
+    if (G.one_device) {
+        for (int p = 0; p < W; ++p)
+            for (int q = 0; q < W; ++q) {
+                const int64_t n = (int64_t)G.shard[p]->out_chunk[q].size;
+                if (q == p || !n) continue;
+                HIP_TRY(hipMemcpyAsync(static_cast<char*>(G.recv[q]) + G.shard[q]->in_off[p],
+                                       static_cast<char*>(G.send[p]) + G.shard[p]->out_off[q], (size_t)n,
+                                       hipMemcpyDeviceToDevice, G.shared));
+            }
+        return GP_OK;
+    }
+    RCCL_TRY(ncclGroupStart());
+    for (int p = 0; p < W; ++p) {
+        const Handle* s = G.shard[p];
+        for (int q = 0; q < W; ++q) {
+            if (q == p) continue;
+            const size_t ns = s->out_chunk[q].size, nr = s->in_chunk[q].size;
+            if (ns) RCCL_TRY(ncclSend(static_cast<char*>(G.send[p]) + s->out_off[q], ns, ncclUint8, q, G.comm[p], s->stream));
+            if (nr) RCCL_TRY(ncclRecv(static_cast<char*>(G.recv[p]) + s->in_off[q], nr, ncclUint8, q, G.comm[p], s->stream));
+        }
+    }
+    RCCL_TRY(ncclGroupEnd());
+    return GP_OK;
+}
+
+int group_sync(Group& G, std::vector<gp_status>& sts) {
+    sts.assign((size_t)G.W, gp_status{});
+    int rc;
+    for (int p = 0; p < G.W; ++p) {
+        if (!G.one_device) HIP_TRY(hipSetDevice(G.dev[p]));
+        if ((rc = shard_sync(G.shard[p], &sts[(size_t)p]))) return rc;
+    }
+    for (int p = 1; p < G.W; ++p)
+        if (sts[p].round != sts[0].round || sts[p].completed != sts[0].completed || sts[p].converged != sts[0].converged)
+            return fail(GP_ESTATE, "shards disagree after round %lld (rank %d)", (long long)sts[0].round, p);
+    G.rounds = sts[0].round;
+    G.completed = sts[0].completed;
+    G.converged = sts[0].converged != 0;
+    return GP_OK;
+}
+
+int group_step(Handle* h, int64_t max_rounds, gp_status* st) {
+    if (max_rounds < 0) return fail(GP_EINVAL, "max_rounds < 0");
+    Group& G = *h->grp;
+    if (G.one_device) HIP_TRY(hipSetDevice(G.dev[0]));
+    const auto t0 = std::chrono::steady_clock::now();
+    const int64_t goal = G.rounds + max_rounds;
+    std::vector<gp_status> sts;
+    int rc;
+    // gossip's F(k) reports round k-1: a batch may run past the convergence round; those
+    // rounds are no-ops on the device (gated) and the counts stay final
+    while (!G.converged && G.rounds < goal) {
+        const int64_t B = std::min<int64_t>(G.batch, goal - G.rounds);
+        for (int64_t i = 0; i < B; ++i) {
+            for (int p = 0; p < G.W; ++p) {
+                if (!G.one_device) HIP_TRY(hipSetDevice(G.dev[p]));
+                if ((rc = shard_round(G.shard[p], G.send[p]))) return rc;
+            }
+            if ((rc = group_exchange(G))) return rc;
+            for (int p = 0; p < G.W; ++p) {
+                if (!G.one_device) HIP_TRY(hipSetDevice(G.dev[p]));
+                if ((rc = shard_deliver(G.shard[p], G.recv[p]))) return rc;
+            }
+        }
+        if ((rc = group_sync(G, sts))) return rc;
+        G.batch = std::min<int64_t>(G.batch * 2, 64);
+    }
+    if (sts.empty() && (rc = group_sync(G, sts))) return rc;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (st) {
+        std::memset(st, 0, sizeof *st);
+        st->round = G.rounds;
+        st->completed = G.completed;
+        st->converged = G.converged ? 1 : 0;
+        st->device_ms = ms;
+        for (const gp_status& s : sts) {  // rank order
+            st->sum_s += s.sum_s;
+            st->sum_w += s.sum_w;
+        }
+    }
+    return GP_OK;
+}
+
+int group_reset(Handle* h) {
+    Group& G = *h->grp;
+    int rc;
+    for (int p = 0; p < G.W; ++p) {
+        if (!G.one_device) HIP_TRY(hipSetDevice(G.dev[p]));
+        if ((rc = reset(G.shard[p]))) return rc;
+    }
+    G.batch = 8;
+    G.rounds = G.completed = 0;
+    G.converged = false;
+    return GP_OK;
+}
+
+int group_create(const gp_config* cfg, gp_layout* out, void** handle) {
+    const int W = std::max(1, cfg->num_gpus);
+    if (W > kMaxWorld) return fail(GP_EINVAL, "num_gpus %d above %d", W, kMaxWorld);
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    auto* grp = new Group();
+    auto* h = new Handle();
+    h->grp = grp;
+    auto bail = [&](int code) {
+        delete grp;
+        h->grp = nullptr;
+        delete h;
+        return code;
+    };
+    Group& G = *grp;
+    G.W = W;
+    G.one_device = (cfg->flags & GP_FLAG_ONE_DEVICE) != 0;
+    for (int p = 0; p < W; ++p) {
+        const int d = G.one_device ? cfg->device : cfg->device + p;
+        if (d < 0 || d >= ndev)
+            return bail(fail(GP_EINVAL, "num_gpus %d from device %d: device %d not present (%d devices)", W,
+                             cfg->device, d, ndev));
+        G.dev.push_back(d);
+    }
+    if (G.one_device) {
+        HIP_TRY(hipSetDevice(cfg->device));
+        hipError_t e = hipStreamCreateWithFlags(&G.shared, hipStreamNonBlocking);
+        if (e != hipSuccess) return bail(fail(GP_EHIP, "hipStreamCreate: %s", hipGetErrorString(e)));
+    }
+    int rc;
+    G.shard.assign((size_t)W, nullptr);
+    G.send.assign((size_t)W, nullptr);
+    G.recv.assign((size_t)W, nullptr);
+    int64_t bytes = 0;
+    for (int p = 0; p < W; ++p) {
+        gp_config c = *cfg;
+        c.device = G.dev[p];
+        c.num_gpus = 0;
+        c.flags &= ~(GP_FLAG_ONE_DEVICE | GP_FLAG_GROUP | GP_FLAG_USE_STREAM);
+        c.stream = nullptr;
+        if (G.one_device) {
+            c.flags |= GP_FLAG_USE_STREAM;
+            c.stream = G.shared;
+        }
+        void* sh = nullptr;
+        gp_layout lay{};
+        if ((rc = create(&c, p, W, true, &lay, nullptr, &sh))) return bail(rc);
+        Handle* s = H(sh);
+        G.shard[p] = s;
+        HIP_TRY(hipSetDevice(G.dev[p]));
+        if (s->send_total && hipMalloc(&G.send[p], (size_t)s->send_total) != hipSuccess)
+            return bail(fail(GP_ENOMEM, "exchange send buffer of %lld bytes", (long long)s->send_total));
+        if (s->recv_total && hipMalloc(&G.recv[p], (size_t)s->recv_total) != hipSuccess)
+            return bail(fail(GP_ENOMEM, "exchange receive buffer of %lld bytes", (long long)s->recv_total));
+        bytes += lay.device_bytes + s->send_total + s->recv_total;
+        if (p == 0) h->lay = lay;
+    }
+    if (!G.one_device) {
+        G.comm.assign((size_t)W, nullptr);
+        ncclResult_t r = ncclCommInitAll(G.comm.data(), W, G.dev.data());
+        if (r != ncclSuccess) {
+            G.comm.clear();
+            return bail(fail(GP_ERCCL, "ncclCommInitAll(%d devices): %s", W, ncclGetErrorString(r)));
+        }
+    }
+    h->cfg = *cfg;
+    h->lay.device_bytes = bytes;
+    h->gossip = G.shard[0]->gossip;
+    h->lo = 0;
+    h->hi = (uint32_t)h->lay.actors;
+    if (out) *out = h->lay;
+    *handle = h;
+    return GP_OK;
+}
+
+// Shard p's part [a, b) of the actor range [first, first + count), or false.
+bool shard_part(const Group& G, int p, int64_t first, int64_t count, int64_t& a, int64_t& b) {
+    a = std::max<int64_t>(first, G.shard[p]->lo);
+    b = std::min<int64_t>(first + count, G.shard[p]->hi);
+    return a < b;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1012,11 +1287,17 @@ int gp_sizes(int64_t n_arg, int32_t topology, int64_t* nodes, int64_t* actors, i
 
 
 int gp_create(const gp_config* cfg, gp_layout* out, void** handle) {
+    if (!cfg || !handle) return fail(GP_EINVAL, "null argument");
+    if (cfg->num_gpus > 1 || (cfg->flags & GP_FLAG_GROUP)) {
+        *handle = nullptr;
+        return group_create(cfg, out, handle);
+    }
     return create(cfg, 0, 1, false, out, nullptr, handle);
 }
 
 int gp_create_shard(const gp_config* cfg, int32_t rank, int32_t world, gp_layout* out, gp_shard_layout* shard,
                     void** handle) {
+    if (cfg && cfg->num_gpus > 1) return fail(GP_EINVAL, "a shard is one GPU (num_gpus %d)", cfg->num_gpus);
     return create(cfg, rank, world, true, out, shard, handle);
 }
 
@@ -1060,17 +1341,34 @@ int gp_shard_sync(void* handle, gp_status* st) {
 
 int gp_reset(void* handle) {
     if (!handle) return fail(GP_EINVAL, "null handle");
+    if (H(handle)->grp) return group_reset(H(handle));
     return reset(H(handle));
 }
 
 int gp_step(void* handle, int64_t max_rounds, gp_status* st) {
     if (!handle) return fail(GP_EINVAL, "null handle");
+    if (H(handle)->grp) return group_step(H(handle), max_rounds, st);
     return step(H(handle), max_rounds, st);
 }
 
 int gp_read_gossip(void* handle, int64_t first, int64_t count, uint32_t* cnt, uint8_t* flags) {
     if (!handle) return fail(GP_EINVAL, "null handle");
     Handle* h = H(handle);
+    if (h->grp) {  // the shards' parts in rank order
+        if (!h->gossip) return fail(GP_ESTATE, "not a gossip handle");
+        int rc = check_range(h, first, count);
+        if (rc) return rc;
+        const Group& G = *h->grp;
+        for (int p = 0; p < G.W; ++p) {
+            int64_t a, b;
+            if (!shard_part(G, p, first, count, a, b)) continue;
+            if (!G.one_device) HIP_TRY(hipSetDevice(G.dev[p]));
+            if ((rc = gp_read_gossip(G.shard[p], a, b - a, cnt ? cnt + (a - first) : nullptr,
+                                     flags ? flags + (a - first) : nullptr)))
+                return rc;
+        }
+        return GP_OK;
+    }
     if (!h->gossip) return fail(GP_ESTATE, "not a gossip handle");
     int rc = check_range(h, first, count);
     if (rc) return rc;
@@ -1083,6 +1381,22 @@ int gp_read_gossip(void* handle, int64_t first, int64_t count, uint32_t* cnt, ui
 int gp_read_pushsum(void* handle, int64_t first, int64_t count, double* S, double* W, uint8_t* flags) {
     if (!handle) return fail(GP_EINVAL, "null handle");
     Handle* h = H(handle);
+    if (h->grp) {
+        if (h->gossip) return fail(GP_ESTATE, "not a push-sum handle");
+        int rc = check_range(h, first, count);
+        if (rc) return rc;
+        const Group& G = *h->grp;
+        for (int p = 0; p < G.W; ++p) {
+            int64_t a, b;
+            if (!shard_part(G, p, first, count, a, b)) continue;
+            if (!G.one_device) HIP_TRY(hipSetDevice(G.dev[p]));
+            const int64_t o = a - first;
+            if ((rc = gp_read_pushsum(G.shard[p], a, b - a, S ? S + o : nullptr, W ? W + o : nullptr,
+                                      flags ? flags + o : nullptr)))
+                return rc;
+        }
+        return GP_OK;
+    }
     if (h->gossip) return fail(GP_ESTATE, "not a push-sum handle");
     int rc = check_range(h, first, count);
     if (rc) return rc;
@@ -1109,6 +1423,22 @@ int gp_read_pushsum(void* handle, int64_t first, int64_t count, double* S, doubl
 int gp_read_messages(void* handle, int64_t first, int64_t count, uint32_t* dst, double* s, double* w) {
     if (!handle) return fail(GP_EINVAL, "null handle");
     Handle* h = H(handle);
+    if (h->grp) {
+        if (h->gossip) return fail(GP_ESTATE, "not a push-sum handle");
+        int rc = check_range(h, first, count);
+        if (rc) return rc;
+        const Group& G = *h->grp;
+        for (int p = 0; p < G.W; ++p) {
+            int64_t a, b;
+            if (!shard_part(G, p, first, count, a, b)) continue;
+            if (!G.one_device) HIP_TRY(hipSetDevice(G.dev[p]));
+            const int64_t o = a - first;
+            if ((rc = gp_read_messages(G.shard[p], a, b - a, dst ? dst + o : nullptr, s ? s + o : nullptr,
+                                       w ? w + o : nullptr)))
+                return rc;
+        }
+        return GP_OK;
+    }
     if (h->gossip) return fail(GP_ESTATE, "not a push-sum handle");
     int rc = check_range(h, first, count);
     if (rc) return rc;
@@ -1122,16 +1452,12 @@ int gp_read_messages(void* handle, int64_t first, int64_t count, uint32_t* dst, 
             if ((rc = copy_slice(h, t, (const uint32_t*)h->tgt, first, count))) return rc;
         } else {
             std::vector<uint8_t> d;
-            std::vector<uint32_t> lk;
             if ((rc = copy_slice(h, d, (const uint8_t*)h->dir[last & 1], first, count))) return rc;
-            if (h->g.has_link) {
-                const int64_t n = std::max<int64_t>(0, std::min<int64_t>(first + count, h->lay.nodes) - first);
-                lk.assign((size_t)count, 0u);
-                if (n > 0) HIP_TRY(hipMemcpy(lk.data(), h->link + first, (size_t)n * 4, hipMemcpyDeviceToHost));
-            }
-            for (int64_t i = 0; i < count; ++i)
+            for (int64_t i = 0; i < count; ++i) {
+                const uint32_t v = (uint32_t)(first + i);
                 t[i] = d[i] == kDirNone ? kNone
-                                        : dir_target(h->g, (uint32_t)(first + i), d[i], h->g.has_link ? lk[i] : 0u);
+                       : dir_target(h->g, v, d[i], d[i] == kDirLink ? link_of(h->cfg.seed, v, (uint32_t)h->lay.nodes) : 0u);
+            }
         }
     }
     for (int64_t i = 0; i < count; ++i) {
@@ -1145,6 +1471,10 @@ int gp_read_messages(void* handle, int64_t first, int64_t count, uint32_t* dst, 
 int gp_read_trace(void* handle, int64_t first_round, int64_t count, int64_t* completed) {
     if (!handle || !completed) return fail(GP_EINVAL, "null argument");
     Handle* h = H(handle);
+    if (h->grp) {  // every shard holds the global count
+        if (!h->grp->one_device) HIP_TRY(hipSetDevice(h->grp->dev[0]));
+        h = h->grp->shard[0];
+    }
     if (first_round < 0 || count < 0 || first_round + count > h->rounds)
         return fail(GP_EINVAL, "trace range outside the %lld executed rounds", (long long)h->rounds);
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1156,6 +1486,10 @@ int gp_read_trace(void* handle, int64_t first_round, int64_t count, int64_t* com
 int gp_neighbors(void* handle, int64_t v, uint32_t* out, int32_t cap) {
     if (!handle) return fail(GP_EINVAL, "null handle");
     Handle* h = H(handle);
+    if (h->grp) {  // the topology is global on every shard
+        if (!h->grp->one_device) HIP_TRY(hipSetDevice(h->grp->dev[0]));
+        h = h->grp->shard[0];
+    }
     if (v < 0 || v >= (int64_t)h->g.actors) return fail(GP_EINVAL, "actor %lld out of range", (long long)v);
     if (h->full) {  // program.fs:201-206: every j != i in ascending order
         const int64_t d = h->lay.nodes;
@@ -1163,8 +1497,7 @@ int gp_neighbors(void* handle, int64_t v, uint32_t* out, int32_t cap) {
         return (int)d;
     }
     const uint32_t m = presence(h->g, (uint32_t)v);
-    uint32_t lk = 0;
-    if (m & 64u) HIP_TRY(hipMemcpy(&lk, h->link + v, 4, hipMemcpyDeviceToHost));
+    const uint32_t lk = (m & 64u) ? link_of(h->cfg.seed, (uint32_t)v, (uint32_t)h->lay.nodes) : 0u;
     int d = 0;
     for (uint32_t c = 0; c < 7; ++c)
         if (m & (1u << c)) {
@@ -1177,6 +1510,7 @@ int gp_neighbors(void* handle, int64_t v, uint32_t* out, int32_t cap) {
 int gp_kernel_stats(void* handle, gp_kstats* out, int32_t reset_counters) {
     if (!handle || !out) return fail(GP_EINVAL, "null argument");
     Handle* h = H(handle);
+    if (h->grp) h = h->grp->shard[0];  // rank 0's kernels
     std::memset(out, 0, sizeof *out);
     out->launches = h->k_launches;
     out->total_ms = h->k_total_ms;
@@ -1193,7 +1527,14 @@ int gp_kernel_stats(void* handle, gp_kstats* out, int32_t reset_counters) {
     return GP_OK;
 }
 
-void gp_destroy(void* handle) { delete H(handle); }
+void gp_destroy(void* handle) {
+    Handle* h = H(handle);
+    if (h && h->grp) {
+        delete h->grp;
+        h->grp = nullptr;
+    }
+    delete h;
+}
 
 const char* gp_last_error(void) { return g_err.c_str(); }
 

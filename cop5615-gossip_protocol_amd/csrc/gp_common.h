@@ -66,6 +66,12 @@ __host__ __device__ __forceinline__ uint32_t philox_x(uint32_t v, uint32_t r, ui
 // Random().Next(0, n) replacement: floor(x * n / 2^32).
 __host__ __device__ __forceinline__ uint32_t scale_draw(uint32_t x, uint32_t n) { return mulhi32(x, n); }
 
+// Imp3D extra link of wired node v: Random().Next(0, nodes-1), i.e. [0, nodes-2] (program.fs:309).
+// A pure function of (seed, v): no rank stores the link array, each recomputes what it needs.
+__host__ __device__ __forceinline__ uint32_t link_of(uint64_t seed, uint32_t v, uint32_t nodes) {
+    return scale_draw(philox_x(v, 0u, kStreamTopo, seed), nodes - 1u);
+}
+
 // ---------------------------------------------------------------- topology
 enum Topology { kLine = 0, kFull = 1, kTwoD = 2, kImp3D = 3, kThreeD = 4 };
 

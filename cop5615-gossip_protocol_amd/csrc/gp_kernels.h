@@ -16,6 +16,19 @@ constexpr int kMaxWorld = 16;
 constexpr uint32_t kSub = 16;
 constexpr uint32_t kCtrStride = 32;  // u32 words between counters
 
+// Push-sum tile kernel (k_ps_tile): each lane owns kTileK consecutive actors, a workgroup one
+// tile of kTileActors; tiles are dealt XCD-contiguously (tile_of_block).
+constexpr uint32_t kTileK = 4;
+constexpr uint32_t kTileActors = kBlock * kTileK;
+
+// Push-sum link-slot marks carry their round: the pass after F(r) writes link_tag(r) into the
+// CSR slot of every actor whose round-r message took its extra link, into the array of parity
+// r & 1; F(r+1) reads a slot as fired iff it holds link_tag(r).  One array sees 255 distinct
+// tags before a value repeats, and it is cleared (hipMemsetAsync) right before that happens
+// (tag_clear_round), so no consumer ever clears a slot and no stale mark can match.
+__host__ __device__ inline uint8_t link_tag(uint32_t r) { return (uint8_t)((r >> 1) % 255u + 1u); }
+__host__ __device__ inline bool tag_clear_round(uint32_t r) { return r >= 2u && (r >> 1) % 255u == 0u; }
+
 // One synchronous round kernel F(r) fuses phase 2 of round r-1 (collect the messages sent to
 // this actor, read from the round r-1 buffers) with phase 1 of round r (update, convergence
 // test, emit).  Buffers ping-pong on r & 1.
@@ -23,6 +36,10 @@ struct RoundArgs {
     Geom g;
     uint64_t seed;
     uint32_t lo, hi;       // actors this kernel updates: [0, actors), or a shard's node range
+    uint32_t tile0;        // first actor of tile 0 (lo rounded down to kTileK)
+    uint32_t ntiles;       // tiles covering [tile0, hi)
+    uint32_t tag_prev;     // link_tag(r - 1): marks of the messages collected by F(r)
+    uint32_t tag_cur;      // link_tag(r): marks written for the messages F(r) emits
     uint32_t slot_lo;      // first link slot held here (0, or the shard's first): the in-bounds
                            // fallback index of predicated-off link-slot loads
     uint32_t sharded;      // completion counts come from the exchange (total[] is global)
@@ -34,17 +51,17 @@ struct RoundArgs {
     uint32_t threshold;    // gossip report threshold (program.fs:102)
     double delta;          // push-sum delta (program.fs:187)
     uint32_t term_limit;   // program.fs:135
-    uint32_t ablate;       // DEBUG ONLY (env GP_ABLATE): bits skip work for cost attribution; results invalid
+    uint32_t ps_tags;      // push-sum: link marks are round tags (link_tag); gossip: chain counts
     unsigned long long* total;  // total[a] = completion count after round a (trace)
     uint32_t* parts;            // kPartRing x kParts padded sub-counters of newly reported actors
     // topology side data (Imp3D)
-    const uint32_t* link;     // extra link per wired node (program.fs:309)
     const uint32_t* rev_off;  // CSR of link sources per destination, ascending
     const uint32_t* rev_src;
     const uint32_t* lpos;     // CSR slot of v's own link edge: rev_src[lpos[v]] == v
-    // Link counts per CSR slot (k_link_count or the exchange; ping-pong; emptied by the
-    // receiver): gossip chains, or push-sum messages that took their link (the receiver then
-    // reads msg_prev[u]; a shard's remote sender's row is written by the exchange).
+    // Link marks per CSR slot, written by k_link_count or the exchange (ping-pong on r & 1):
+    // gossip: the chains that took the link (emptied by the receiver); push-sum: link_tag(r)
+    // when the sender's round-r message took it (the receiver then reads msg_prev[u]; a
+    // shard's remote sender's message is written into rmsg by the exchange).
     uint8_t* lcnt_prev;
     uint8_t* lcnt_cur;
     // push-sum state
@@ -137,7 +154,7 @@ int grid_for(uint32_t n);
 uint32_t span_for(uint32_t n, int grid);
 
 // round kernels
-void launch_ps_pull(const RoundArgs& a, const Launch& l);
+void launch_ps_tile(const RoundArgs& a, const Launch& l);
 void launch_gs_pull(const RoundArgs& a, const Launch& l);
 void launch_link_count(const RoundArgs& a, const Launch& l);
 void launch_ps_push_emit(const RoundArgs& a, const Launch& l);
@@ -156,16 +173,17 @@ void launch_shard_pack(const RoundArgs& a, const Xchg& x, long long applied, hip
 void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, uint32_t max_cap, int gossip,
                          int full, hipStream_t s);
 // per-(source rank, destination rank, degree) counts of extra links, for the exchange plan
-void launch_link_hist(const uint32_t* link, const Geom& g, const Xchg& x, unsigned long long* hist,
-                      const Launch& l);
+void launch_link_hist(uint64_t seed, const Geom& g, const Xchg& x, unsigned long long* hist, const Launch& l);
 
 // setup / utility kernels
-void launch_links(uint32_t* link, uint32_t nodes, uint64_t seed, const Launch& l);
-void launch_count(const uint32_t* idx, uint32_t n, uint32_t* counts, const Launch& l);
-void launch_rev_fill(const uint32_t* link, uint32_t nodes, const uint32_t* rev_off, uint32_t* fillc,
-                     uint32_t* rev_src, const Launch& l);
+// extra-link CSR construction (links recomputed by link_of)
+void launch_dst_count(uint64_t seed, uint32_t nodes, uint32_t ulo, uint32_t uhi, uint32_t* counts, const Launch& l);
+void launch_dst_fill(uint64_t seed, uint32_t nodes, uint32_t ulo, uint32_t uhi, uint32_t tlo, uint32_t thi,
+                     const uint32_t* off, uint32_t* fill, uint32_t* out, const Launch& l);
+void launch_add_u32(uint32_t* x, const uint32_t* y, uint32_t n, const Launch& l);
 void launch_sort_segments(const uint32_t* off, uint32_t* vals, uint32_t n, const Launch& l);
-void launch_lpos(const uint32_t* rev_src, uint32_t nlinks, uint32_t* lpos, const Launch& l);
+void launch_lpos_lists(const uint32_t* off, const uint32_t* list, uint32_t nt, const uint32_t* base, uint32_t* lpos,
+                       const Launch& l);
 // exclusive scan of n u32 counts into off[0..n]; scratch >= scan_scratch_words(n) u32
 size_t scan_scratch_words(uint32_t n);
 void launch_exclusive_scan(const uint32_t* in, uint32_t* off, uint32_t n, uint32_t* scratch, hipStream_t s);

@@ -140,137 +140,302 @@ __device__ __forceinline__ T load_sel(const T* base, bool pred, uint32_t idx, ui
     return base[pred ? idx : fallback];
 }
 
-// Link slots scanned with unrolled loads before the (rare) tail loop.
+// Link slots scanned with unrolled loads before the (rare) tail loop (gossip pull).
 constexpr uint32_t kLinkUnroll = 4;
 
+// Whole-dword / 16-byte loads at byte-granular addresses: gfx950 serves unaligned global loads
+// (tools/microbench/unaligned.hip), so a row of 4 direction bytes or 16 link marks that starts at
+// an arbitrary actor or slot id is one load instruction.
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
+__device__ __forceinline__ uint2 ld_u64(const uint8_t* p) { return *reinterpret_cast<const uint2*>(p); }
+__device__ __forceinline__ uint4 ld_u128(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ uint32_t byte_of(uint32_t w, uint32_t i) { return (w >> (8u * i)) & 0xFFu; }
 
-// One actor's round (program.fs:119-143 after collecting the round r-1 messages to v).
-// Collect = the canonical sequential fp64 sum, from +0.0, of the messages sent to v in ascending
-// source id.  Messages are never copied on one GPU: a message IS the sender's held state, so a
-// grid sender's message is read from msg_prev at v-G^2, v-G, v-1, v+1, v+G or v+G^2 (a sender
-// targets v iff its direction byte is the opposite code), and an extra-link sender u (CSR
-// rev_src, ascending) from msg_prev[u] iff k_link_count marked u's CSR slot.  Loads are
-// unconditional (clamped addresses) in three dependency levels: (1) own flags, held (S,W), the
-// six neighbours' direction bytes, the CSR range; (2) the first 3 grid hits' messages and, per
-// CSR slot of the first kLinkUnroll, the source id and link count (coalesced: CSR order);
-// (3) the messages of the links that fired.
-// LM: 0 no extra links; 1 links; 2 links on a shard of several ranks: a sender outside [lo, hi)
-// is remote, and the exchange wrote its message into the receiver's slot, rmsg_prev[slot].
-template <int LM>
-__global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
-    if (gate(a, a.r)) return;
-    const Geom g = a.g;
-    const uint32_t r = a.r;
-    uint32_t v, end, step;
-    node_range(a.lo, a.hi, a.span, v, end, step);
-    uint32_t newly = 0;
-    for (; v < end; v += step) {
-        const uint32_t m = presence(g, v);
-        if (m) {
-        const uint32_t code = (a.ablate & 8u) ? kth_bit(m, v % popc(m))
-                                              : kth_bit(m, scale_draw(philox_x(v, r, kStreamPush, a.seed), popc(m)));
-        uint8_t f = a.flags[v];
-        double2 held = make_double2((double)v, 1.0);
-        double ss = 0.0, ww = 0.0;
-        uint32_t cin = 0;
-        if (r) {
-            held = a.msg_prev[v];
-            uint8_t d[6];
+// Tile t of workgroup b: workgroups with equal b % 8 share an XCD under round-robin dispatch
+// (speed only, never correctness), so group x walks the x-th contiguous eighth of the tiles in
+// dispatch order and the rows its tiles re-read (v -+ G, v -+ G^2) stay in that XCD's L2.
+__device__ __forceinline__ uint32_t tile_of_block(uint32_t b, uint32_t nb) { return (b & 7u) * (nb >> 3) + (b >> 3); }
+
+// Presence masks (program.fs:295-306, as presence()) of the 4 consecutive actors v0 .. v0+3:
+// one pair of divisions, then the coordinates step by one actor.
+__device__ __forceinline__ void presence4(const Geom& g, uint32_t v0, uint32_t (&m)[kTileK]) {
+    const uint32_t yz = fdiv(v0, g.dx);
+    uint32_t x = v0 - yz * g.gx;
+    uint32_t z = fdiv(yz, g.dy);
+    uint32_t y = yz - z * g.gy;
 #pragma unroll
-            for (uint32_t k = 0; k < 6; ++k) d[k] = load_sel(a.dir_prev, (m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
-            uint32_t li = 0, nl = 0;
-            if (LM) {
-                li = a.rev_off[v];
-                nl = (a.ablate & 1u) ? 0u : a.rev_off[v + 1] - li;
+    for (uint32_t j = 0; j < kTileK; ++j) {
+        const uint32_t v = v0 + j;
+        uint32_t mm = 0;
+        mm |= (x > 0) ? 1u : 0u;
+        mm |= (x + 1 < g.gx && v + 1 < g.wired) ? 2u : 0u;
+        mm |= (y > 0) ? 4u : 0u;
+        mm |= (y + 1 < g.gy && v + g.gx < g.wired) ? 8u : 0u;
+        mm |= (z > 0) ? 16u : 0u;
+        mm |= (z + 1 < g.gz && v + g.plane < g.wired) ? 32u : 0u;
+        mm |= g.has_link ? 64u : 0u;
+        m[j] = v < g.wired ? mm : 0u;
+        if (++x == g.gx) {
+            x = 0;
+            if (++y == g.gy) {
+                y = 0;
+                ++z;
             }
-            uint32_t hits = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 6; ++k) hits |= ((m & slot_bit(k)) && d[k] == slot_code(k)) ? 1u << k : 0u;
-            if (a.ablate & 16u) hits = 0;
-            uint32_t hk[3], rest = hits;
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                hk[j] = rest ? (uint32_t)__builtin_ctz(rest) : 6u;
-                rest &= rest - 1u;
-            }
-            double2 gm[3];
-#pragma unroll
-            for (int j = 0; j < 3; ++j) gm[j] = load_sel(a.msg_prev, hk[j] < 6u, slot_src(g, v, hk[j] < 6u ? hk[j] : 0u), v);
-            uint32_t gi = 0;
-            auto add = [&](double2 mm) {
-                ss += mm.x;
-                ww += mm.y;
-                ++cin;
-            };
-            auto flush = [&](uint32_t bound) {
-#pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    if (gi == (uint32_t)j && hk[j] < 6u && slot_src(g, v, hk[j]) < bound) {
-                        add(gm[j]);
-                        ++gi;
-                    }
-                if (gi >= 3) {
-                    while (rest) {
-                        const uint32_t k = (uint32_t)__builtin_ctz(rest);
-                        const uint32_t u = slot_src(g, v, k);
-                        if (u >= bound) break;
-                        add(a.msg_prev[u]);
-                        rest &= rest - 1u;
-                    }
-                }
-            };
-            if (LM) {
-                uint32_t ls[kLinkUnroll];
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k) ls[k] = load_sel(a.rev_src, k < nl, li + k, a.slot_lo);
-                bool lk[kLinkUnroll];
-                double2 lm[kLinkUnroll];
-                uint8_t lc[kLinkUnroll];
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, a.slot_lo);
-                // ---- level 3: the messages of the sources whose slot is marked
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k) {
-                    lk[k] = k < nl && lc[k] != 0;
-                    if (lk[k]) a.lcnt_prev[li + k] = 0;
-                    if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) lm[k] = a.rmsg_prev[li + k];
-                    else lm[k] = load_sel(a.msg_prev, lk[k], ls[k], v);
-                }
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k)
-                    if (lk[k]) {
-                        flush(ls[k]);
-                        add(lm[k]);
-                    }
-                for (uint32_t k = kLinkUnroll; k < nl; ++k) {  // rare: more than kLinkUnroll sources
-                    if (a.lcnt_prev[li + k]) {
-                        const uint32_t u = a.rev_src[li + k];
-                        a.lcnt_prev[li + k] = 0;
-                        flush(u);
-                        add(LM == 2 && (u < a.lo || u >= a.hi) ? a.rmsg_prev[li + k] : a.msg_prev[u]);
-                    }
-                }
-            }
-            flush(0xFFFFFFFFu);
         }
-        const uint8_t f0 = f;
-        const PsOut o = ps_update(f, held, ss, ww, cin, a.delta, a.term_limit);
-        // non-temporal: the round's 160 MB of messages cannot stay in L2 until the next round
-        // reads them, and streaming them past it leaves L2 to the +-G, +-G^2 rows read now
-        // (measured ~1.5% per round; non-temporal LOADS of the CSR were 7% slower)
+    }
+}
+
+struct Sum3 {
+    double s, w;
+    uint32_t c;
+};
+
+// Add message mm when `take` holds.  Adding +0.0 otherwise leaves a sum of non-negative terms
+// bit-identical (every s and w is >= +0.0), so the canonical sequence needs no branches.
+__device__ __forceinline__ void add_if(Sum3& a, bool take, double2 mm) {
+    a.s += take ? mm.x : 0.0;
+    a.w += take ? mm.y : 0.0;
+    a.c += take ? 1u : 0u;
+}
+
+// The general collect of one actor (any number of link receipts): the canonical sum of the
+// messages sent to v in round r-1 in ascending source id, everything re-read from memory.  Only
+// lanes the tile kernel's fixed budgets do not cover take it (> 4 fired link slots or > 12 slots
+// in the lane: ~0.05% of lanes at 10M actors).
+template <int LM>
+__device__ __forceinline__ Sum3 collect_general(const RoundArgs& a, uint32_t v, uint32_t m) {
+    const Geom& g = a.g;
+    Sum3 acc{0.0, 0.0, 0u};
+    uint32_t rest = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 6; ++k)
+        if ((m & slot_bit(k)) && a.dir_prev[slot_src(g, v, k)] == slot_code(k)) rest |= 1u << k;
+    auto flush = [&](uint32_t bound) {
+        while (rest) {
+            const uint32_t u = slot_src(g, v, (uint32_t)__builtin_ctz(rest));
+            if (u >= bound) break;
+            add_if(acc, true, a.msg_prev[u]);
+            rest &= rest - 1u;
+        }
+    };
+    if (LM) {
+        const uint32_t li = a.rev_off[v], le = a.rev_off[v + 1];
+        for (uint32_t i = li; i < le; ++i)
+            if (a.lcnt_prev[i] == a.tag_prev) {
+                const uint32_t u = a.rev_src[i];
+                flush(u);
+                add_if(acc, true, (LM == 2 && (u < a.lo || u >= a.hi)) ? a.rmsg_prev[i] : a.msg_prev[u]);
+            }
+    }
+    flush(0xFFFFFFFFu);
+    return acc;
+}
+
+// One push-sum round for the 4 actors v0 .. v0+3 of one lane (program.fs:119-143 after
+// collecting the round r-1 messages sent to each; round 0 = :110-116).  Returns how many of
+// them converged (the ParentActor's PushSumResult count, program.fs:54-60).
+//
+// Collect = the canonical sequential fp64 sum, from +0.0, of the messages sent to v in
+// ascending source id.  A message is never copied: the message a sender emits in round r is its
+// held (S,W) for round r+1, so every message is read from the sender's own row msg_prev[u].
+//   * grid senders (v-G^2, v-G, v-1, v+1, v+G, v+G^2, ascending) target v iff their direction
+//     byte is the opposite code.  The lane reads the 4 direction bytes of each of those rows as
+//     one (unaligned) dword; the -1 / +1 senders of inner actors are the lane's own held rows.
+//   * extra-link senders (Imp3D, program.fs:309) are the ascending CSR rev_src[rev_off[v] ..];
+//     a slot fired iff it holds link_tag(r-1).  The lane's slots are contiguous, so its marks
+//     are one 16-byte load and its sources up to three.  A link message is inserted into the
+//     grid sequence at its source's place (before the first grid sender with a larger id).
+// Loads come in three dependency levels: (1) flags, held rows, direction rows, CSR bounds;
+// (2) grid-hit messages, link marks and sources; (3) fired link messages.
+// LM: 0 no extra links; 1 links; 2 links on a shard of several ranks (a sender outside [lo, hi)
+// is remote: the exchange wrote its message into the receiver's slot, rmsg_prev[slot]).
+template <int LM>
+__device__ __forceinline__ uint32_t ps_tile_lane(const RoundArgs& a, uint32_t v0) {
+    const Geom& g = a.g;
+    const uint32_t r = a.r;
+    uint32_t m[kTileK];
+    presence4(g, v0, m);
+    // actors of this lane inside [lo, hi): j in [ja, jb)
+    const uint32_t ja = v0 < a.lo ? a.lo - v0 : 0u;
+    const uint32_t jb = v0 + kTileK > a.hi ? a.hi - v0 : kTileK;
+#pragma unroll
+    for (uint32_t j = 0; j < kTileK; ++j)
+        if (j < ja || j >= jb) m[j] = 0u;
+    const uint32_t any = m[0] | m[1] | m[2] | m[3];
+    if (!any) return 0u;
+
+    // ---- level 1: flags, held rows, direction rows, CSR bounds
+    const uint32_t F = ld_u32(a.flags + v0);
+    double2 H[kTileK];
+    uint32_t hit[kTileK] = {0u, 0u, 0u, 0u};  // grid receipts, bit k = slot k (ascending source)
+    Sum3 acc[kTileK];
+#pragma unroll
+    for (uint32_t j = 0; j < kTileK; ++j) {
+        H[j] = r ? a.msg_prev[v0 + j] : make_double2((double)(v0 + j), 1.0);
+        acc[j] = Sum3{0.0, 0.0, 0u};
+    }
+    if (r) {
+        const uint32_t P = g.plane, G = g.gx;
+        // signed row offsets: a row below the lane's first actor may start up to 3 bytes before
+        // actor 0 (into the allocation's padding), never at a wrapped-around 32-bit index
+        const int64_t w0 = (int64_t)v0;
+        const uint2 DX = ld_u64(a.dir_prev + (w0 - 2));  // actors v0-2 .. v0+5
+        const uint32_t Dzm = ld_u32(a.dir_prev + ((any & 16u) ? w0 - (int64_t)P : w0));
+        const uint32_t Dym = ld_u32(a.dir_prev + ((any & 4u) ? w0 - (int64_t)G : w0));
+        const uint32_t Dyp = ld_u32(a.dir_prev + ((any & 8u) ? w0 + (int64_t)G : w0));
+        const uint32_t Dzp = ld_u32(a.dir_prev + ((any & 32u) ? w0 + (int64_t)P : w0));
+        uint32_t R[kTileK + 1] = {0u, 0u, 0u, 0u, 0u};
+        if (LM) {
+            const uint4 R4 = ld_u128(a.rev_off + v0);
+            R[0] = R4.x;
+            R[1] = R4.y;
+            R[2] = R4.z;
+            R[3] = R4.w;
+            R[4] = a.rev_off[v0 + kTileK];
+        }
+        auto dx = [&](uint32_t i) { return i < 4u ? byte_of(DX.x, i) : byte_of(DX.y, i - 4u); };
+#pragma unroll
+        for (uint32_t j = 0; j < kTileK; ++j) {
+            const uint32_t mj = m[j];
+            uint32_t h = 0;
+            h |= ((mj & 16u) && byte_of(Dzm, j) == 5u) ? 1u : 0u;   // v-G^2 sent +z
+            h |= ((mj & 4u) && byte_of(Dym, j) == 3u) ? 2u : 0u;    // v-G sent +y
+            h |= ((mj & 1u) && dx(1u + j) == 1u) ? 4u : 0u;         // v-1 sent +x
+            h |= ((mj & 2u) && dx(3u + j) == 0u) ? 8u : 0u;         // v+1 sent -x
+            h |= ((mj & 8u) && byte_of(Dyp, j) == 2u) ? 16u : 0u;   // v+G sent -y
+            h |= ((mj & 32u) && byte_of(Dzp, j) == 4u) ? 32u : 0u;  // v+G^2 sent -z
+            hit[j] = h;
+        }
+
+        // ---- level 2: grid-hit messages (the inner -1 / +1 ones are held rows already)
+        double2 gm[kTileK][6];
+        const int32_t off[6] = {-(int32_t)P, -(int32_t)G, -1, 1, (int32_t)G, (int32_t)P};
+#pragma unroll
+        for (uint32_t j = 0; j < kTileK; ++j)
+#pragma unroll
+            for (uint32_t k = 0; k < 6; ++k) {
+                gm[j][k] = make_double2(0.0, 0.0);
+                if (k == 2 && j > 0) gm[j][k] = H[j - 1];
+                else if (k == 3 && j + 1 < kTileK) gm[j][k] = H[j + 1];
+                else if (hit[j] & (1u << k)) gm[j][k] = a.msg_prev[(uint32_t)((int32_t)(v0 + j) + off[k])];
+            }
+
+        // ---- links: up to 4 fired slots among the lane's first 12, loaded in one go
+        constexpr uint32_t kItems = 4;
+        double2 lmsg[kItems];
+        uint32_t lkey[kItems];  // actor j * 8 + insertion position 0..6; 0xFF: none
+        bool slow = false;
+        if (LM) {
+            // CSR bounds of the lane's actors inside [lo, hi) (entries outside are not ours)
+            uint32_t Rc[kTileK + 1];
+#pragma unroll
+            for (uint32_t j = 0; j <= kTileK; ++j) Rc[j] = R[j < ja ? ja : (j > jb ? jb : j)];
+            const uint32_t S0 = Rc[0], n = Rc[kTileK] - Rc[0];
+            const uint4 MK = ld_u128(a.lcnt_prev + S0);
+            const uint4 U0 = ld_u128(a.rev_src + S0);
+            uint4 U1 = make_uint4(0u, 0u, 0u, 0u), U2 = U1;
+            if (n > 4) U1 = ld_u128(a.rev_src + S0 + 4);
+            if (n > 8) U2 = ld_u128(a.rev_src + S0 + 8);
+            const uint32_t tag4 = a.tag_prev * 0x01010101u;
+            const uint32_t mk[4] = {MK.x ^ tag4, MK.y ^ tag4, MK.z ^ tag4, MK.w ^ tag4};
+            uint32_t fired = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 16; ++i) fired |= (byte_of(mk[i >> 2], i & 3u) == 0u && i < n) ? 1u << i : 0u;
+            slow = n > 12u || __builtin_popcount(fired) > (int)kItems;
+            const uint32_t U[12] = {U0.x, U0.y, U0.z, U0.w, U1.x, U1.y, U1.z, U1.w, U2.x, U2.y, U2.z, U2.w};
+            uint32_t rest = fired;
+#pragma unroll
+            for (uint32_t q = 0; q < kItems; ++q) {
+                const bool valid = rest != 0u && !slow;
+                const uint32_t i = valid ? (uint32_t)__builtin_ctz(rest) : 0u;
+                rest &= rest - 1u;
+                uint32_t u = U[0];
+#pragma unroll
+                for (uint32_t t = 1; t < 12; ++t) u = i == t ? U[t] : u;
+                const uint32_t slot = S0 + i;
+                const uint32_t j = (slot >= Rc[1] ? 1u : 0u) + (slot >= Rc[2] ? 1u : 0u) + (slot >= Rc[3] ? 1u : 0u);
+                const uint32_t vq = v0 + j;
+                // grid senders of vq with a smaller id than u (slots that do not exist never
+                // carry a message, so counting them is harmless); u + d > vq  <=>  u > vq - d
+                const uint32_t pos = (u + P > vq ? 1u : 0u) + (u + G > vq ? 1u : 0u) + (u + 1u > vq ? 1u : 0u) +
+                                     (u > vq + 1u ? 1u : 0u) + (u > vq + G ? 1u : 0u) + (u > vq + P ? 1u : 0u);
+                lkey[q] = valid ? j * 8u + pos : 0xFFu;
+                // ---- level 3: the fired link's message
+                lmsg[q] = make_double2(0.0, 0.0);
+                if (valid) lmsg[q] = (LM == 2 && (u < a.lo || u >= a.hi)) ? a.rmsg_prev[slot] : a.msg_prev[u];
+            }
+        } else {
+#pragma unroll
+            for (uint32_t q = 0; q < kItems; ++q) {
+                lkey[q] = 0xFFu;
+                lmsg[q] = make_double2(0.0, 0.0);
+            }
+        }
+
+        // ---- the canonical sums: per actor, links before / between / after the grid senders
+        bool inner = false;  // a link source strictly between two of an actor's grid senders
+#pragma unroll
+        for (uint32_t q = 0; q < kItems; ++q) inner |= lkey[q] != 0xFFu && (lkey[q] & 7u) != 0u && (lkey[q] & 7u) != 6u;
+        const bool any_inner = __any(inner);
+#pragma unroll
+        for (uint32_t j = 0; j < kTileK; ++j) {
+            Sum3& s = acc[j];
+#pragma unroll
+            for (uint32_t q = 0; q < kItems; ++q) add_if(s, lkey[q] == j * 8u, lmsg[q]);
+#pragma unroll
+            for (uint32_t k = 0; k < 6; ++k) {
+                if (k > 0 && any_inner) {
+#pragma unroll
+                    for (uint32_t q = 0; q < kItems; ++q) add_if(s, lkey[q] == j * 8u + k, lmsg[q]);
+                }
+                add_if(s, (hit[j] >> k) & 1u, gm[j][k]);
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < kItems; ++q) add_if(s, lkey[q] == j * 8u + 6u, lmsg[q]);
+        }
+        if (LM && slow) {
+#pragma unroll
+            for (uint32_t j = 0; j < kTileK; ++j)
+                if (m[j]) acc[j] = collect_general<LM>(a, v0 + j, m[j]);
+        }
+    }
+
+    // ---- update + emit (program.fs:119-143), one Philox draw per actor
+    uint32_t Fn = F, D = 0x01010101u * kDirNone, newly = 0;  // kDirNone in every byte
+#pragma unroll
+    for (uint32_t j = 0; j < kTileK; ++j) {
+        if (!m[j]) continue;
+        const uint32_t v = v0 + j;
+        uint8_t f = (uint8_t)byte_of(F, j);
+        const uint32_t code = kth_bit(m[j], scale_draw(philox_x(v, r, kStreamPush, a.seed), popc(m[j])));
+        const PsOut o = ps_update(f, H[j], acc[j].s, acc[j].w, acc[j].c, a.delta, a.term_limit);
+        // non-temporal: the round's messages cannot stay in L2 until the next round reads them
         if (o.send) {
             __builtin_nontemporal_store(o.msg.x, &a.msg_cur[v].x);
             __builtin_nontemporal_store(o.msg.y, &a.msg_cur[v].y);
         }
-        __builtin_nontemporal_store(o.send ? (uint8_t)code : kDirNone, &a.dir_cur[v]);
-        if (f != f0) a.flags[v] = f;
+        D = (D & ~(0xFFu << (8u * j))) | ((o.send ? code : (uint32_t)kDirNone) << (8u * j));
+        Fn = (Fn & ~(0xFFu << (8u * j))) | ((uint32_t)f << (8u * j));
         if (o.conv_now) {
             a.frozen[v] = o.msg;
             ++newly;
         }
-        }
     }
-    block_add(newly, a.parts, r);
+    // whole dwords: bytes of actors outside [lo, hi) are the halo rows (rewritten by the
+    // exchange after this kernel) or padding; flags outside keep the value read
+    __builtin_nontemporal_store(D, reinterpret_cast<uint32_t*>(a.dir_cur + v0));
+    if (Fn != F) *reinterpret_cast<uint32_t*>(a.flags + v0) = Fn;
+    return newly;
+}
+
+template <int LM>
+__global__ __launch_bounds__(kBlock) void k_ps_tile(RoundArgs a) {
+    if (gate(a, a.r)) return;
+    const uint32_t t = tile_of_block(blockIdx.x, gridDim.x);
+    const uint32_t v0 = a.tile0 + t * kTileActors + threadIdx.x * kTileK;
+    uint32_t newly = 0;
+    if (t < a.ntiles && v0 < a.hi) newly = ps_tile_lane<LM>(a, v0);
+    block_add(newly, a.parts, a.r);
 }
 
 // ------------------------------------------------------------------ gossip, grid topologies
@@ -352,8 +517,15 @@ __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
 // slot indices in flight together, then the scattered stores.
 constexpr uint32_t kScatterPer = 4;
 
+// Past convergence when the round before the one F(r) applied already reached the target:
+// F(r) applies round r (push-sum) or r - 1 (gossip) and publishes the count before it.
+__device__ __forceinline__ bool applied_converged(const RoundArgs& a) {
+    const long long ap = a.ps_tags ? (long long)a.r : (long long)a.r - 1;
+    return ap >= 1 && a.total[ap - 1] >= a.target;
+}
+
 __global__ __launch_bounds__(kBlock) void k_link_count(RoundArgs a) {
-    if (a.r >= 1 && a.total[a.r - 1] >= a.target) return;  // past convergence (F(r) published it)
+    if (applied_converged(a)) return;
     const uint32_t n = a.g.wired;
     const uint32_t base = blockIdx.x * kBlock * kScatterPer + threadIdx.x;
     uint32_t nl[kScatterPer], lp[kScatterPer];
@@ -367,7 +539,7 @@ __global__ __launch_bounds__(kBlock) void k_link_count(RoundArgs a) {
     for (uint32_t j = 0; j < kScatterPer; ++j) lp[j] = load_sel(a.lpos, nl[j] != 0u, base + j * kBlock, 0u);
 #pragma unroll
     for (uint32_t j = 0; j < kScatterPer; ++j)
-        if (nl[j]) a.lcnt_cur[lp[j]] = (uint8_t)nl[j];
+        if (nl[j]) a.lcnt_cur[lp[j]] = (uint8_t)(a.ps_tags ? a.tag_cur : nl[j]);
 }
 
 // ------------------------------------------------------------------ shard exchange
@@ -428,6 +600,7 @@ constexpr uint32_t kShardPer = 4;
 // count (the receiver reads msg_prev[u] itself, as on one GPU); one whose slot belongs to another
 // rank goes to that rank's send chunk as (global slot, s, w), written into the same slot there.
 __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg x) {
+    if (applied_converged(a)) return;  // block-uniform: F(r) was a no-op
     const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
     const uint32_t base = a.lo + blockIdx.x * kBlock * kShardPer + threadIdx.x;
     const uint32_t slo = x.sbnd[x.rank], shi = x.sbnd[x.rank + 1];
@@ -452,7 +625,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg 
     uint32_t q[kShardPer], pos[kShardPer];
 #pragma unroll
     for (uint32_t j = 0; j < kShardPer; ++j) {
-        if (l[j] && !rm[j]) a.lcnt_cur[lp[j]] = 1;
+        if (l[j] && !rm[j]) a.lcnt_cur[lp[j]] = (uint8_t)a.tag_cur;
         q[j] = rm[j] ? owner(x.sbnd, x.world, lp[j]) : 0u;
     }
     block_reserve(x, rm, q, pos);
@@ -462,6 +635,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg 
 }
 
 __global__ __launch_bounds__(kBlock) void k_gs_link_scatter_x(RoundArgs a, Xchg x) {
+    if (applied_converged(a)) return;  // block-uniform
     const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
     const uint32_t base = a.lo + blockIdx.x * kBlock * kShardPer + threadIdx.x;
     const uint32_t slo = x.sbnd[x.rank], shi = x.sbnd[x.rank + 1];
@@ -507,6 +681,7 @@ __device__ __forceinline__ uint32_t block_reserve1(uint32_t* ctr, bool want) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_shard_halo(RoundArgs a, Xchg x, int pushsum) {
+    if (applied_converged(a)) return;  // block-uniform; the chunks' headers still go out (pack)
     for (int side = 0; side < 2; ++side) {
         const uint32_t n = x.h.out_n[side];
         const uint32_t first = x.h.out_first[side], code = x.h.code[side], cap = x.h.out_cap[side];
@@ -643,20 +818,20 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
             else if (gossip) a.lcnt_cur[t] = (uint8_t)((e >> 31) + 1u);
             else {  // the sender's message into the receiver's slot, the slot marked
                 a.rmsg_cur[t] = in.msg[i];
-                a.lcnt_cur[t] = 1;
+                a.lcnt_cur[t] = (uint8_t)a.tag_cur;
             }
         }
     }
 }
 
 // hist[(src rank * world + dst rank) * 8 + degree] over every extra link (LDS-privatised).
-__global__ __launch_bounds__(kBlock) void k_link_hist(const uint32_t* link, Geom g, Xchg x, unsigned long long* hist) {
+__global__ __launch_bounds__(kBlock) void k_link_hist(uint64_t seed, Geom g, Xchg x, unsigned long long* hist) {
     __shared__ uint32_t h[kMaxWorld * kMaxWorld * 8];
     const uint32_t nb = x.world * x.world * 8;
     for (uint32_t i = threadIdx.x; i < nb; i += kBlock) h[i] = 0;
     __syncthreads();
     for (uint32_t u = blockIdx.x * kBlock + threadIdx.x; u < g.wired; u += gridDim.x * kBlock) {
-        const uint32_t sp = owner(x.abnd, x.world, u), dp = owner(x.abnd, x.world, link[u]);
+        const uint32_t sp = owner(x.abnd, x.world, u), dp = owner(x.abnd, x.world, link_of(seed, u, g.wired));
         atomicAdd(&h[(sp * x.world + dp) * 8 + popc(presence(g, u))], 1u);
     }
     __syncthreads();
@@ -677,7 +852,7 @@ __device__ __forceinline__ uint32_t generic_deg(const RoundArgs& a, uint32_t v, 
 __device__ __forceinline__ uint32_t generic_target(const RoundArgs& a, uint32_t v, uint32_t m, uint32_t idx) {
     if (a.full) return idx + (idx >= v ? 1u : 0u);
     const uint32_t code = kth_bit(m, idx);
-    return dir_target(a.g, v, code, code == kDirLink ? a.link[v] : 0u);
+    return dir_target(a.g, v, code, code == kDirLink ? link_of(a.seed, v, a.nodes) : 0u);
 }
 
 // Gossip on any topology (used for "full"): receipts are integer atomics into inc_cur[t]
@@ -822,23 +997,32 @@ __global__ __launch_bounds__(kBlock) void k_ps_push_fill(RoundArgs a, uint32_t* 
 }
 
 // ------------------------------------------------------------------ setup / utility kernels
-__global__ void k_links(uint32_t* link, uint32_t nodes, uint64_t seed) {
-    // program.fs:309: Random().Next(0, nodes-1) -> [0, nodes-2]
-    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < nodes; v += gridDim.x * blockDim.x)
-        link[v] = scale_draw(philox(v, 0u, kStreamTopo, seed).x, nodes - 1u);
+// ---- extra-link CSR construction (Imp3D, program.fs:309): links recomputed by link_of()
+// counts[link_of(u)] += 1 for the senders u in [ulo, uhi)
+__global__ void k_dst_count(uint64_t seed, uint32_t nodes, uint32_t ulo, uint32_t uhi, uint32_t* counts) {
+    for (uint32_t u = ulo + blockIdx.x * blockDim.x + threadIdx.x; u < uhi; u += gridDim.x * blockDim.x)
+        atomicAdd(&counts[link_of(seed, u, nodes)], 1u);
 }
 
-__global__ void k_count(const uint32_t* idx, uint32_t n, uint32_t* counts) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        atomicAdd(&counts[idx[i]], 1u);
-}
-
-__global__ void k_rev_fill(const uint32_t* link, uint32_t nodes, const uint32_t* rev_off, uint32_t* fillc,
-                           uint32_t* rev_src) {
-    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < nodes; v += gridDim.x * blockDim.x) {
-        const uint32_t t = link[v];
-        rev_src[rev_off[t] + atomicAdd(&fillc[t], 1u)] = v;
+// out[off[t] + k] = u for the senders u in [ulo, uhi) whose destination t lies in [tlo, thi)
+// (k from fill[t]: unordered; k_sort_segments restores ascending sources)
+__global__ void k_dst_fill(uint64_t seed, uint32_t nodes, uint32_t ulo, uint32_t uhi, uint32_t tlo, uint32_t thi,
+                           const uint32_t* off, uint32_t* fill, uint32_t* out) {
+    for (uint32_t u = ulo + blockIdx.x * blockDim.x + threadIdx.x; u < uhi; u += gridDim.x * blockDim.x) {
+        const uint32_t t = link_of(seed, u, nodes);
+        if (t >= tlo && t < thi) out[off[t] + atomicAdd(&fill[t], 1u)] = u;
     }
+}
+
+__global__ void k_add_u32(uint32_t* x, const uint32_t* y, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) x[i] += y[i];
+}
+
+// lpos[u] = base[t] + (p - off[t]) for every position p of destination t's list of senders:
+// a sender's global CSR slot = its destination's first slot + the senders before it
+__global__ void k_lpos_lists(const uint32_t* off, const uint32_t* list, uint32_t nt, const uint32_t* base, uint32_t* lpos) {
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x)
+        for (uint32_t p = off[t]; p < off[t + 1]; ++p) lpos[list[p]] = base[t] + (p - off[t]);
 }
 
 __global__ void k_sort_segments(const uint32_t* off, uint32_t* vals, uint32_t n) {
@@ -854,11 +1038,6 @@ __global__ void k_sort_segments(const uint32_t* off, uint32_t* vals, uint32_t n)
             vals[j] = x;
         }
     }
-}
-
-__global__ void k_lpos(const uint32_t* rev_src, uint32_t nlinks, uint32_t* lpos) {
-    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < nlinks; p += gridDim.x * blockDim.x)
-        lpos[rev_src[p]] = p;
 }
 
 constexpr uint32_t kScanPer = 8;
@@ -1002,10 +1181,13 @@ uint32_t span_for(uint32_t n, int grid) {
     return (s + kBlock - 1) / kBlock * kBlock;
 }
 
-void launch_ps_pull(const RoundArgs& a, const Launch& l) {
-    if (!a.g.has_link) hipLaunchKernelGGL(k_ps_pull<0>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
-    else if (a.rmsg_prev) hipLaunchKernelGGL(k_ps_pull<2>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
-    else hipLaunchKernelGGL(k_ps_pull<1>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+// One workgroup per tile, a multiple of 8 of them (tile_of_block); the ones past the last tile
+// only take part in the gate and the count.
+void launch_ps_tile(const RoundArgs& a, const Launch& l) {
+    const dim3 grid((a.ntiles + 7u) / 8u * 8u);
+    if (!a.g.has_link) hipLaunchKernelGGL(k_ps_tile<0>, grid, dim3(kBlock), 0, l.stream, a);
+    else if (a.rmsg_prev) hipLaunchKernelGGL(k_ps_tile<2>, grid, dim3(kBlock), 0, l.stream, a);
+    else hipLaunchKernelGGL(k_ps_tile<1>, grid, dim3(kBlock), 0, l.stream, a);
 }
 
 void launch_gs_pull(const RoundArgs& a, const Launch& l) {
@@ -1068,30 +1250,31 @@ void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, u
     hipLaunchKernelGGL(k_shard_unpack, dim3(bpp * x.world), dim3(kBlock), 0, s, a, x, applied, gossip, full);
 }
 
-void launch_link_hist(const uint32_t* link, const Geom& g, const Xchg& x, unsigned long long* hist,
-                      const Launch& l) {
-    hipLaunchKernelGGL(k_link_hist, dim3(l.grid), dim3(kBlock), 0, l.stream, link, g, x, hist);
+void launch_link_hist(uint64_t seed, const Geom& g, const Xchg& x, unsigned long long* hist, const Launch& l) {
+    hipLaunchKernelGGL(k_link_hist, dim3(l.grid), dim3(kBlock), 0, l.stream, seed, g, x, hist);
 }
 
-void launch_links(uint32_t* link, uint32_t nodes, uint64_t seed, const Launch& l) {
-    hipLaunchKernelGGL(k_links, dim3(l.grid), dim3(kBlock), 0, l.stream, link, nodes, seed);
+void launch_dst_count(uint64_t seed, uint32_t nodes, uint32_t ulo, uint32_t uhi, uint32_t* counts, const Launch& l) {
+    if (uhi > ulo) hipLaunchKernelGGL(k_dst_count, dim3(l.grid), dim3(kBlock), 0, l.stream, seed, nodes, ulo, uhi, counts);
 }
 
-void launch_count(const uint32_t* idx, uint32_t n, uint32_t* counts, const Launch& l) {
-    hipLaunchKernelGGL(k_count, dim3(l.grid), dim3(kBlock), 0, l.stream, idx, n, counts);
+void launch_dst_fill(uint64_t seed, uint32_t nodes, uint32_t ulo, uint32_t uhi, uint32_t tlo, uint32_t thi,
+                     const uint32_t* off, uint32_t* fill, uint32_t* out, const Launch& l) {
+    if (uhi > ulo)
+        hipLaunchKernelGGL(k_dst_fill, dim3(l.grid), dim3(kBlock), 0, l.stream, seed, nodes, ulo, uhi, tlo, thi, off, fill, out);
 }
 
-void launch_rev_fill(const uint32_t* link, uint32_t nodes, const uint32_t* rev_off, uint32_t* fillc,
-                     uint32_t* rev_src, const Launch& l) {
-    hipLaunchKernelGGL(k_rev_fill, dim3(l.grid), dim3(kBlock), 0, l.stream, link, nodes, rev_off, fillc, rev_src);
+void launch_add_u32(uint32_t* x, const uint32_t* y, uint32_t n, const Launch& l) {
+    hipLaunchKernelGGL(k_add_u32, dim3(l.grid), dim3(kBlock), 0, l.stream, x, y, n);
+}
+
+void launch_lpos_lists(const uint32_t* off, const uint32_t* list, uint32_t nt, const uint32_t* base, uint32_t* lpos,
+                       const Launch& l) {
+    hipLaunchKernelGGL(k_lpos_lists, dim3(l.grid), dim3(kBlock), 0, l.stream, off, list, nt, base, lpos);
 }
 
 void launch_sort_segments(const uint32_t* off, uint32_t* vals, uint32_t n, const Launch& l) {
     hipLaunchKernelGGL(k_sort_segments, dim3(l.grid), dim3(kBlock), 0, l.stream, off, vals, n);
-}
-
-void launch_lpos(const uint32_t* rev_src, uint32_t nlinks, uint32_t* lpos, const Launch& l) {
-    hipLaunchKernelGGL(k_lpos, dim3(l.grid), dim3(kBlock), 0, l.stream, rev_src, nlinks, lpos);
 }
 
 size_t scan_scratch_words(uint32_t n) { return (n + kScanTile - 1) / kScanTile + 1; }

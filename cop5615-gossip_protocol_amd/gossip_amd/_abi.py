@@ -13,20 +13,22 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, os.environ.get("GP_LIB", "lib"), "libgossip_hip.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "gossip_hip.h")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 TOPOLOGIES = {"line": 0, "full": 1, "2D": 2, "Imp3D": 3, "3D": 4}
 ALGOS = {"gossip": 0, "push-sum": 1}
 FLAG_KERNEL_TIMING = 1
 FLAG_GENERIC = 2
 FLAG_USE_STREAM = 4
-ERRORS = {-1: "GP_EINVAL", -2: "GP_ENOMEM", -3: "GP_EHIP", -4: "GP_ESTATE", -5: "GP_EOVERFLOW"}
+FLAG_ONE_DEVICE = 8
+FLAG_GROUP = 16
+ERRORS = {-1: "GP_EINVAL", -2: "GP_ENOMEM", -3: "GP_EHIP", -4: "GP_ESTATE", -5: "GP_EOVERFLOW", -6: "GP_ERCCL"}
 
 
 class Config(C.Structure):
     _fields_ = [("n_arg", C.c_int64), ("topology", C.c_int32), ("algo", C.c_int32),
                 ("seed", C.c_uint64), ("delta", C.c_double), ("gossip_threshold", C.c_int32),
                 ("term_init", C.c_int32), ("term_limit", C.c_int32), ("device", C.c_int32),
-                ("flags", C.c_int32), ("reserved", C.c_int32), ("stream", C.c_void_p)]
+                ("flags", C.c_int32), ("num_gpus", C.c_int32), ("stream", C.c_void_p)]
 
 
 class Layout(C.Structure):

@@ -185,9 +185,45 @@ class LoopbackTransport:
                 eq.recv_buf[ro[q][p]:ro[q][p] + n].copy_(ep.send_buf[so[p][q]:so[p][q] + n])
 
 
-def run(engine, transport, max_rounds: int = 1 << 40, batch: int = 8, max_batch: int = 64):
+class PhaseTimer:
+    """Per-phase device time of one rank's rounds, from events on the stream the engine runs on
+    (torch's current stream): every `every`-th round is bracketed as round (the round kernel, the
+    link scatter, the halo and the chunk headers) | exchange (the all-to-all) | deliver (unpack)."""
+
+    def __init__(self, every: int = 8):
+        import torch
+
+        self.torch = torch
+        self.every = every
+        self.pending = []
+        self.n = 0
+        self.ms = {"round": 0.0, "exchange": 0.0, "deliver": 0.0}
+        self.count = 0
+
+    def events(self):
+        self.count += 1
+        if (self.count - 1) % self.every:
+            return None
+        ev = [self.torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        self.pending.append(ev)
+        return ev
+
+    def collect(self):
+        for ev in self.pending:
+            ev[3].synchronize()
+            for k, (a, b) in zip(("round", "exchange", "deliver"), zip(ev[:3], ev[1:])):
+                self.ms[k] += a.elapsed_time(b)
+            self.n += 1
+        self.pending = []
+
+    def means(self):
+        return {k + "_ms": (v / self.n if self.n else None) for k, v in self.ms.items()}
+
+
+def run(engine, transport, max_rounds: int = 1 << 40, batch: int = 8, max_batch: int = 64, timer=None):
     """Advance this rank until the GLOBAL count reaches `nodes` (program.fs:49,56) or
-    max_rounds rounds; every rank of the job must call it with the same arguments."""
+    max_rounds rounds; every rank of the job must call it with the same arguments.  timer: a
+    PhaseTimer (sampled per-phase event timing)."""
     st = engine.sync()
     goal = int(st.round) + max_rounds
     while not st.converged and st.round < goal:
@@ -195,10 +231,21 @@ def run(engine, transport, max_rounds: int = 1 << 40, batch: int = 8, max_batch:
         # a convergence; rounds issued beyond it are no-ops on the device (gated).
         b = min(batch, goal - int(st.round))
         for _ in range(b):
+            ev = timer.events() if timer else None
+            if ev:
+                ev[0].record()
             engine.round()
+            if ev:
+                ev[1].record()
             transport.exchange(engine)
+            if ev:
+                ev[2].record()
             engine.deliver()
+            if ev:
+                ev[3].record()
         st = engine.sync()
+        if timer:
+            timer.collect()
         batch = min(batch * 2, max_batch)
     return st
 

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 2
+#define GP_ABI_VERSION 3
 
 /* program.fs:151 "line", :191 "full", :227 "2D", :267 "Imp3D"; "3D" is build-defined (Q9) */
 enum gp_topology { GP_LINE = 0, GP_FULL = 1, GP_TWO_D = 2, GP_IMP3D = 3, GP_THREE_D = 4 };
@@ -39,12 +39,16 @@ enum gp_error {
     GP_EHIP = -3,   /* a HIP runtime call failed                         */
     GP_ESTATE = -4, /* call not valid in the handle's current state      */
     GP_EOVERFLOW = -5, /* a shard's fixed-capacity message buffer overflowed (results void) */
+    GP_ERCCL = -6,  /* an RCCL call failed (num_gpus > 1)                  */
 };
 
 enum gp_flags {
-    GP_FLAG_KERNEL_TIMING = 1, /* hipEvent kernel timing (gp_kernel_stats): gp_step brackets groups of 8 rounds (or every 8th kernel when a pass follows it), a shard every round */
+    GP_FLAG_KERNEL_TIMING = 1, /* hipEvent kernel timing (gp_kernel_stats): gp_step brackets groups of 8 rounds (or every 8th kernel when a pass follows it); a shard brackets every 8th round */
     GP_FLAG_GENERIC = 2,       /* force the generic bucketed push path on grid topologies    */
     GP_FLAG_USE_STREAM = 4,    /* run on cfg->stream even when it is NULL (the null stream)  */
+    GP_FLAG_ONE_DEVICE = 8,    /* num_gpus > 1: every shard on cfg->device, exchange by device
+                                  copies on one stream (tests the multi-GPU engine on one GPU) */
+    GP_FLAG_GROUP = 16,        /* use the multi-GPU engine (shards + RCCL) also at num_gpus = 1 */
 };
 
 typedef struct gp_config {
@@ -56,11 +60,15 @@ typedef struct gp_config {
     int32_t gossip_threshold; /* program.fs:102 (10)                                    */
     int32_t term_init;        /* program.fs:79 (1)                                      */
     int32_t term_limit;       /* program.fs:135 (3)                                     */
-    int32_t device;           /* HIP device ordinal                                     */
+    int32_t device;           /* HIP device ordinal (the first one when num_gpus > 1)    */
     int32_t flags;            /* gp_flags                                               */
-    int32_t reserved;
+    int32_t num_gpus;         /* 0 or 1: one GPU.  N > 1: one graph split into N node-range
+                                 shards on devices device .. device+N-1 inside this process;
+                                 the library owns one stream per device and the RCCL
+                                 communicators (ncclCommInitAll), and exchanges each round
+                                 with grouped ncclSend / ncclRecv     */
     void* stream;             /* hipStream_t to run on; NULL without GP_FLAG_USE_STREAM:
-                                 a library-owned stream                                  */
+                                 a library-owned stream (ignored when num_gpus > 1)      */
 } gp_config;
 
 typedef struct gp_layout {
@@ -100,7 +108,9 @@ int gp_sizes(int64_t n_arg, int32_t topology, int64_t* nodes, int64_t* actors, i
 
 /* Replaces the topology builders + actor spawn + InitializeVariables + leader pick
  * (program.fs:150-175, 191-211, 227-252, 267-317).  Builds the implicit topology and the
- * Imp3D extra-link CSR on the device and initialises the protocol state. */
+ * Imp3D extra-link CSR on the device and initialises the protocol state.  With
+ * cfg->num_gpus = N > 1 the handle is one graph over N GPUs of this process: gp_step, gp_reset,
+ * gp_read_*, gp_kernel_stats and gp_destroy act on all of them (reads may span shards). */
 int gp_create(const gp_config* cfg, gp_layout* out, void** handle);
 
 /* Re-initialise protocol state (same topology/links) so a run can be repeated. */
@@ -108,7 +118,8 @@ int gp_reset(void* handle);
 
 /* Replaces the actor message loop (ChildActor, program.fs:82-146) and the ParentActor
  * termination count (program.fs:44-63): advance at most max_rounds synchronous rounds, or
- * until completed >= nodes. */
+ * until completed >= nodes.  device_ms is the round loop's time: hipEvents on one GPU, the
+ * host clock around the loop (every GPU drained) for num_gpus > 1. */
 int gp_step(void* handle, int64_t max_rounds, gp_status* st);
 
 /* State read-back (the caller owns the host buffers; any pointer may be NULL). */

@@ -68,3 +68,33 @@ def test_cli_argument_contract():
     assert r.returncode == 2
     r = subprocess.run([exe, "100"], capture_output=True, text=True)
     assert r.returncode == 2
+    r = subprocess.run([exe, "100", "line", "gossip", "--mode", "async"], capture_output=True, text=True)
+    assert r.returncode == 2 and "--mode async" in r.stderr  # only the round engine is built
+    r = subprocess.run([exe, "100", "line", "gossip", "--quiet"], capture_output=True, text=True)
+    assert r.returncode == 2  # unknown option
+
+
+def test_config_struct_layout():
+    """gp_config as the header lays it out (ABI 3: num_gpus in the former reserved slot), so a
+    P/Invoke / ctypes mirror built from the header agrees field by field."""
+    import ctypes as C
+
+    text = open(_abi.HEADER).read()
+    assert "int32_t num_gpus;" in text and "reserved" not in text
+    assert [f[0] for f in _abi.Config._fields_] == [
+        "n_arg", "topology", "algo", "seed", "delta", "gossip_threshold", "term_init", "term_limit",
+        "device", "flags", "num_gpus", "stream"]
+    assert C.sizeof(_abi.Config) == 64 and _abi.Config.num_gpus.offset == 52 and _abi.Config.stream.offset == 56
+    for name, val in (("GP_FLAG_ONE_DEVICE", 8), ("GP_FLAG_GROUP", 16), ("GP_ERCCL", -6)):
+        assert re.search(rf"{name}\s*=\s*{val}\b", text), name
+    assert (_abi.FLAG_ONE_DEVICE, _abi.FLAG_GROUP, _abi.ERRORS[-6]) == (8, 16, "GP_ERCCL")
+
+
+def test_library_links_rccl():
+    """Multi-GPU lives behind the ABI: the library itself links RCCL (ncclCommInitAll, grouped
+    ncclSend / ncclRecv) rather than leaving the exchange to the host."""
+    out = subprocess.run(["readelf", "-d", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    assert "librccl.so" in out
+    und = subprocess.run(["nm", "-D", "--undefined-only", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    for sym in ("ncclCommInitAll", "ncclSend", "ncclRecv", "ncclGroupStart", "ncclGroupEnd"):
+        assert sym in und, sym

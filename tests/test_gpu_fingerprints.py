@@ -75,3 +75,14 @@ def test_shards_vs_fingerprint(name, world):
     _check(fp, sts[0], engines[0].read_trace(), _shard_arrays(engines, fp["algorithm"]))
     for e in engines:
         e.close()
+
+
+@pytest.mark.parametrize("name,world", [("C3_imp3d_10m_pushsum", 8), ("C4_full_100m_gossip", 8)])
+def test_group_vs_fingerprint(name, world):
+    """The same decomposition behind the C ABI (gp_config.num_gpus, the library's own exchange),
+    all shards on this GPU."""
+    fp = FP[name]
+    sim = Simulator(fp["n_arg"], fp["topology"], fp["algorithm"], seed=fp["seed"], num_gpus=world, one_device=True)
+    st = sim.step(_cap(fp))
+    _check(fp, st, sim.read_trace(), state_arrays(sim, fp["algorithm"]), sim.layout)
+    sim.close()

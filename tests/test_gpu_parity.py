@@ -128,6 +128,7 @@ def test_cli_report_and_trace(tmp_path):
     """The drop-in CLI (program.fs:19-21 argv, :51-52 report) on the GPU: banner, convergence
     report and rounds, and --trace's per-round count curve equal to the oracle's."""
     import os
+    import re
     import subprocess
 
     exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -137,11 +138,20 @@ def test_cli_report_and_trace(tmp_path):
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     lines = r.stdout.splitlines()
-    assert lines[0] == "Push Sum Started"  # program.fs:322
-    assert any(x.startswith("Convergence Time: ") and x.endswith(" ms") for x in lines)
     cpu = oracle.OracleSim(1000, "Imp3D", "push-sum", seed=3)
     cs = cpu.step()
-    assert f"Rounds: {cs.round}" in lines
+    # exactly the reference's lines (program.fs:322, :51-52) plus the round count
+    assert len(lines) == 4, lines
+    assert lines[0] == "Push Sum Started"
+    assert lines[1] == "-" * 59
+    assert re.fullmatch(r"Convergence Time: \d+\.\d{6} ms", lines[2]), lines[2]
+    assert lines[3] == f"Rounds: {cs.round}"
+    # --verbose adds the layout line after the banner; --gpus 1 / --mode round change nothing
+    r = subprocess.run([exe, "1000", "Imp3D", "push-sum", "--seed", "3", "--verbose", "--gpus", "1", "--mode", "round"],
+                       capture_output=True, text=True, timeout=60)
+    v = r.stdout.splitlines()
+    assert r.returncode == 0 and len(v) == 5 and v[1].startswith("actors 1001 (nodes 1000), leader ")
+    assert v[0] == lines[0] and v[4] == lines[3]
     rows = np.loadtxt(out, delimiter=",", skiprows=1, dtype=np.int64).reshape(-1, 2)
     np.testing.assert_array_equal(rows[:, 0], np.arange(cs.round))
     np.testing.assert_array_equal(rows[:, 1], cpu.read_trace())

@@ -20,7 +20,7 @@ kt() {  # $1 = output name, rest = command
   local n=$1; shift
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 ${KT_TIMEOUT:-240} rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$n" -o kt -- "$@" > "$O/$n.log" 2>&1 )
   rc=$?; echo "kt $n rc=$rc"; tail -1 "$O/$n.log"; [ $rc -eq 0 ] || return $rc
-  python3 "$R/tools/kt_summary.py" "$O/$n/kt_kernel_trace.csv" | head -${KT_LINES:-6}
+  python3 "$R/tools/kt_summary.py" "$O/$n/kt_kernel_trace.csv" > "$O/$n.summary" && head -n ${KT_LINES:-6} "$O/$n.summary"
 }
 case $MODE in
   tests) tests ;;
