@@ -198,8 +198,6 @@ struct Handle {
         a.seed = cfg.seed;
         a.lo = lo;
         a.hi = hi;
-        a.tile0 = lo & ~(kTileK - 1u);
-        a.ntiles = (hi - a.tile0 + kTileActors - 1u) / kTileActors;
         a.tag_prev = r ? link_tag(r - 1u) : 0u;
         a.tag_cur = link_tag(r);
         a.ps_tags = gossip ? 0u : 1u;
@@ -326,7 +324,7 @@ int build_links(Handle* h) {
     if (!h->generic) {  // pull kernels
         // per-slot link marks of the own slots (gossip chains, push-sum round tags)
         if ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))) return rc;
-        // a remote sender's link message lands in the receiver's slot, read in CSR order (k_ps_tile<2>)
+        // a remote sender's link message lands in the receiver's slot, read in CSR order (k_ps_pull<2>)
         if (h->sharded && h->world > 1 && !h->gossip &&
             ((rc = h->alloc(&h->rmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->rmsg[1], (size_t)nsl, slo))))
             return rc;
@@ -431,15 +429,17 @@ int reset(Handle* h) {
     return GP_OK;
 }
 
+bool fused_marks(const Handle* h) { return kFuseLinkMarks && !h->gossip && !h->generic && !h->sharded && h->g.has_link; }
+
 const char* round_kernel_name(const Handle* h) {
     if (h->gossip) return h->generic ? "k_gs_push" : (h->g.has_link ? "k_gs_pull<true>" : "k_gs_pull<false>");
     if (h->generic) return "k_ps_push_emit";
-    return h->g.has_link ? (h->rmsg[0] ? "k_ps_tile<2>" : "k_ps_tile<1>") : "k_ps_tile<0>";
+    return h->g.has_link ? (h->rmsg[0] ? "k_ps_pull<2>" : "k_ps_pull<1>") : "k_ps_pull<0>";
 }
 
 const char* aux_kernel_name(const Handle* h) {
     if (h->generic) return h->gossip ? "" : "k_scan_* + k_ps_push_fill";
-    if (!h->g.has_link) return "";
+    if (!h->g.has_link || fused_marks(h)) return "";
     if (h->sharded) return h->gossip ? "k_gs_link_scatter_x" : "k_ps_link_scatter_x";
     return "k_link_count";
 }
@@ -466,6 +466,16 @@ double bytes_per_round(const Handle* h) {
     return b;
 }
 
+// Push-sum link marks of round r go into lcnt[r & 1]; clear that array before a tag value
+// repeats in it (link_tag), after F(r-1) has read it and before round r's marks are written
+// (by F(r) itself when the marks are fused, else by the pass after it).
+int clear_tags_if_due(Handle* h, uint32_t r) {
+    if (h->gossip || !h->lcnt[0] || !tag_clear_round(r)) return GP_OK;
+    const int64_t slo = h->sbnd[h->rank], ns = h->sbnd[h->rank + 1] - slo;
+    HIP_TRY(hipMemsetAsync(h->lcnt[r & 1u] + slo, 0, (size_t)ns, h->stream));
+    return GP_OK;
+}
+
 // The dominant round kernel F(k) (timed under GP_FLAG_KERNEL_TIMING) ...
 void launch_main(Handle* h, int64_t k, const Xchg* x) {
     const RoundArgs a = h->args((uint32_t)k);
@@ -480,7 +490,7 @@ void launch_main(Handle* h, int64_t k, const Xchg* x) {
     } else if (h->generic) {
         launch_ps_push_emit(a, l);
     } else {
-        launch_ps_tile(a, l);
+        launch_ps_pull(a, l);
     }
 }
 
@@ -489,10 +499,8 @@ int launch_aux(Handle* h, int64_t k, const Xchg* x) {
     const uint32_t r = (uint32_t)k;
     const RoundArgs a = h->args(r);
     const Launch l = h->L();
-    if (!h->gossip && h->lcnt[0] && tag_clear_round(r)) {  // this parity's tags are about to repeat
-        const int64_t slo = h->sbnd[h->rank], ns = h->sbnd[h->rank + 1] - slo;
-        HIP_TRY(hipMemsetAsync(h->lcnt[r & 1u] + slo, 0, (size_t)ns, h->stream));
-    }
+    int rc;
+    if (!fused_marks(h) && (rc = clear_tags_if_due(h, r))) return rc;
     if (h->gossip) {
         if (!h->generic && h->g.has_link) {
             if (x) launch_gs_link_scatter_x(a, *x, l);
@@ -504,7 +512,7 @@ int launch_aux(Handle* h, int64_t k, const Xchg* x) {
         launch_ps_push_fill(a, h->slot[c], h->boff[c], l);
     } else if (h->g.has_link) {
         if (x) launch_ps_link_scatter_x(a, *x, l);
-        else launch_link_count(a, l);
+        else if (!fused_marks(h)) launch_link_count(a, l);
     }
     return GP_OK;
 }
@@ -522,10 +530,11 @@ int ensure_events(Handle* h, int64_t rounds) {
 
 // Round k with its three timing events (slot i of the event ring).
 int launch_round(Handle* h, int64_t k, const Xchg* x, bool timing, int64_t i) {
+    int rc;
+    if (fused_marks(h) && (rc = clear_tags_if_due(h, (uint32_t)k))) return rc;
     if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i], h->stream));
     launch_main(h, k, x);
     if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i + 1], h->stream));
-    int rc;
     if ((rc = launch_aux(h, k, x))) return rc;
     if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i + 2], h->stream));
     return GP_OK;

@@ -16,10 +16,12 @@ constexpr int kMaxWorld = 16;
 constexpr uint32_t kSub = 16;
 constexpr uint32_t kCtrStride = 32;  // u32 words between counters
 
-// Push-sum tile kernel (k_ps_tile): each lane owns kTileK consecutive actors, a workgroup one
-// tile of kTileActors; tiles are dealt XCD-contiguously (tile_of_block).
-constexpr uint32_t kTileK = 4;
-constexpr uint32_t kTileActors = kBlock * kTileK;
+// Single-GPU Imp3D push-sum: the round kernel writes the link marks of its own messages (no
+// k_link_count pass; 1% faster than the separate pass at 10M).  GP_FUSE_LINK=0: the pass.
+#ifndef GP_FUSE_LINK
+#define GP_FUSE_LINK 1
+#endif
+constexpr bool kFuseLinkMarks = GP_FUSE_LINK != 0;
 
 // Push-sum link-slot marks carry their round: the pass after F(r) writes link_tag(r) into the
 // CSR slot of every actor whose round-r message took its extra link, into the array of parity
@@ -36,8 +38,6 @@ struct RoundArgs {
     Geom g;
     uint64_t seed;
     uint32_t lo, hi;       // actors this kernel updates: [0, actors), or a shard's node range
-    uint32_t tile0;        // first actor of tile 0 (lo rounded down to kTileK)
-    uint32_t ntiles;       // tiles covering [tile0, hi)
     uint32_t tag_prev;     // link_tag(r - 1): marks of the messages collected by F(r)
     uint32_t tag_cur;      // link_tag(r): marks written for the messages F(r) emits
     uint32_t slot_lo;      // first link slot held here (0, or the shard's first): the in-bounds
@@ -154,7 +154,7 @@ int grid_for(uint32_t n);
 uint32_t span_for(uint32_t n, int grid);
 
 // round kernels
-void launch_ps_tile(const RoundArgs& a, const Launch& l);
+void launch_ps_pull(const RoundArgs& a, const Launch& l);
 void launch_gs_pull(const RoundArgs& a, const Launch& l);
 void launch_link_count(const RoundArgs& a, const Launch& l);
 void launch_ps_push_emit(const RoundArgs& a, const Launch& l);

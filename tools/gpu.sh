@@ -34,10 +34,13 @@ case $MODE in
     rc=$?; echo "bench rc=$rc"; cat "$O/bench.json"; [ $rc -eq 0 ] || exit $rc
     kt kt python3 "$R/bench.py" --no-cpu-baseline ${BENCH_ARGS} ;;
   pmc)
+    # one rocprofv3 run per pass; counters of one pass joined by commas in $PMC_EXTRA
     for c in FETCH_SIZE WRITE_SIZE ${PMC_EXTRA}; do
-      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_$c" -o p -- python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-60} ${PROF_ARGS} > "$O/pmc_$c.log" 2>&1 )
+      n=${c%%,*}
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --pmc ${c//,/ } --output-format csv -d "$O/pmc_$n" -o p -- python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-60} ${PROF_ARGS} > "$O/pmc_$n.log" 2>&1 )
       rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
-    done ;;
+    done
+    python3 "$R/tools/pmc_summary.py" "$O" > "$O/summary.txt" 2>&1; cat "$O/summary.txt" ;;
   ab)
     for v in ${VARIANTS}; do
       GP_LIB=lib_$v kt "kt_$v" python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-300} ${PROF_ARGS} || exit $?

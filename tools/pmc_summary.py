@@ -11,6 +11,7 @@ agg = defaultdict(list)
 for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if pat in r["Kernel_Name"]:
-            agg[(r["Kernel_Name"].split("(")[0][-40:], r["Counter_Name"])].append(float(r["Counter_Value"]))
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
+            agg[(name[-40:], r["Counter_Name"])].append(float(r["Counter_Value"]))
 for (k, c), v in sorted(agg.items()):
     print(f"{k:42s} {c:24s} n={len(v):4d} median={statistics.median(v):.6g} (first {v[0]:.6g})")

@@ -1,8 +1,10 @@
-# Build tuning variants of the kernel file into cop5615-gossip_protocol_amd/lib_<name>/ (GP_LIB selects one).
+# Build tuning variants of libgossip_hip.so into cop5615-gossip_protocol_amd/lib_<name>/ (GP_LIB=lib_<name>
+# selects one).  Each argument is NAME:FLAGS, e.g.  k1:-DGP_TILE_K=1  (FLAGS: extra hipcc defines).
 set -e
 R=$(cd "$(dirname "$0")/../.." && pwd); P=$R/cop5615-gossip_protocol_amd
-for f in "$@"; do
-  n=$(basename $f .hip); mkdir -p $P/lib_$n
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -I$R/include -I$P/csrc -shared -o $P/lib_$n/libgossip_hip.so $f $P/csrc/gp_api.cpp &
+for spec in "$@"; do
+  n=${spec%%:*}; f=${spec#*:}; mkdir -p $P/lib_$n
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall $f -I$R/include -I$P/csrc \
+    -shared -o $P/lib_$n/libgossip_hip.so $P/csrc/gp_kernels.hip $P/csrc/gp_api.cpp -L/opt/rocm/lib -lrccl &
 done
 wait
