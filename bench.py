@@ -82,17 +82,21 @@ def workload(args, world):
 
 def pmc_traffic(kernels, wl: str):
     """HBM bytes per round of `kernels` (summed) from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic.json, made by tools/make_pmc_traffic.py), or None."""
+    (profiles/pmc_traffic.json {workload: {kernel: ...}}, made by tools/make_pmc_traffic.py), or
+    None when the workload or a kernel has no entry."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
+    per = d.get(wl)
+    if not isinstance(per, dict):
+        return None
     total = 0.0
     for k in kernels:
-        e = d.get(k)
-        if not e or e.get("workload") != wl:
+        e = per.get(k)
+        if not e:
             return None
         total += e["hbm_bytes_per_launch"]
     return total

@@ -141,7 +141,10 @@ __device__ __forceinline__ T load_sel(const T* base, bool pred, uint32_t idx, ui
 }
 
 // Link slots scanned with unrolled loads before the (rare) tail loop.
-constexpr uint32_t kLinkUnroll = 4;
+#ifndef GP_LINK_UNROLL
+#define GP_LINK_UNROLL 4
+#endif
+constexpr uint32_t kLinkUnroll = GP_LINK_UNROLL;
 
 // Timing-only builds (tools/variants) may drop parts of the round kernel to price them; the
 // product is built with 0, and the results of any other value are wrong by construction.
@@ -175,9 +178,16 @@ constexpr bool kNtStore16 = GP_NT16 != 0;
 // CSR slot of the first kLinkUnroll, the source id and link count (coalesced: CSR order);
 // (3) the messages of the links that fired.
 // LM: 0 no extra links; 1 links; 2 links on a shard of several ranks: a sender outside [lo, hi)
-// is remote, and the exchange wrote its message into the receiver's slot, rmsg_prev[slot].
+// is remote, and the exchange wrote its message into the receiver's slot, rmsg_prev[slot];
+// 3 (kPushLink builds) one GPU, every link message read from the slot the sender copied it to.
+// Waves per SIMD the round kernel is compiled for (VGPR budget 512 / waves): the kernel is
+// latency-bound, so more resident waves = more loads in flight (A/B knob).
+#ifndef GP_PS_WAVES
+#define GP_PS_WAVES 6
+#endif
+
 template <int LM>
-__global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WAVES))) void k_ps_pull(RoundArgs a) {
     if (gate(a, a.r)) return;
     const Geom g = a.g;
     const uint32_t r = a.r;
@@ -248,12 +258,21 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
                 uint8_t lc[kLinkUnroll];
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, a.slot_lo);
+                if constexpr (LM == 3 && kPushLink == 1) {  // slot messages, same level as the marks
+#pragma unroll
+                    for (uint32_t k = 0; k < kLinkUnroll; ++k) lm[k] = load_sel(a.rmsg_prev, k < nl, li + k, a.slot_lo);
+                }
                 // ---- level 3: the messages of the sources whose slot is marked
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) {
                     lk[k] = k < nl && lc[k] == a.tag_prev;  // round-tagged marks: nothing to clear
-                    if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) lm[k] = a.rmsg_prev[li + k];
-                    else lm[k] = load_sel(a.msg_prev, lk[k], ls[k], v);
+                    if constexpr (LM == 3) {
+                        if constexpr (kPushLink != 1) lm[k] = load_sel(a.rmsg_prev, lk[k], li + k, a.slot_lo);
+                    } else if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
+                        lm[k] = a.rmsg_prev[li + k];
+                    } else {
+                        lm[k] = load_sel(a.msg_prev, lk[k], ls[k], v);
+                    }
                 }
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k)
@@ -265,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
                     if (a.lcnt_prev[li + k] == a.tag_prev) {
                         const uint32_t u = a.rev_src[li + k];
                         flush(u);
-                        add(LM == 2 && (u < a.lo || u >= a.hi) ? a.rmsg_prev[li + k] : a.msg_prev[u]);
+                        add(LM == 3 || (LM == 2 && (u < a.lo || u >= a.hi)) ? a.rmsg_prev[li + k] : a.msg_prev[u]);
                     }
                 }
             }
@@ -285,8 +304,12 @@ __global__ __launch_bounds__(kBlock) void k_ps_pull(RoundArgs a) {
             }
         }
         __builtin_nontemporal_store(o.send ? (uint8_t)code : kDirNone, &a.dir_cur[v]);
-        if constexpr (LM == 1 && kFuseLinkMarks) {  // the link pass's mark, written by the sender
-            if (o.send && code == kDirLink) a.lcnt_cur[a.lpos[v]] = (uint8_t)a.tag_cur;
+        if constexpr ((LM == 1 || LM == 3) && kFuseLinkMarks) {  // the link pass's mark, written by the sender
+            if (o.send && code == kDirLink) {
+                const uint32_t p = a.lpos[v];
+                a.lcnt_cur[p] = (uint8_t)a.tag_cur;
+                if constexpr (LM == 3) a.rmsg_cur[p] = o.msg;
+            }
         }
         if (f != f0) a.flags[v] = f;
         if (o.conv_now) {
@@ -1043,6 +1066,7 @@ uint32_t span_for(uint32_t n, int grid) {
 
 void launch_ps_pull(const RoundArgs& a, const Launch& l) {
     if (!a.g.has_link) hipLaunchKernelGGL(k_ps_pull<0>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+    else if (a.rmsg_prev && !a.sharded) hipLaunchKernelGGL(k_ps_pull<3>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
     else if (a.rmsg_prev) hipLaunchKernelGGL(k_ps_pull<2>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
     else hipLaunchKernelGGL(k_ps_pull<1>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
 }

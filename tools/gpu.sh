@@ -6,11 +6,12 @@
 #   bench   the default bench.py line (with the CPU baseline) + its rocprofv3 kernel trace/stats
 #   pmc     FETCH_SIZE and WRITE_SIZE passes (one run each) over 60 rounds of prof_run.py
 #   ab      kernel-trace A/B of the variant libraries named in $VARIANTS (lib_<name>/, GP_LIB)
-# Extra prof_run.py arguments: $PROF_ARGS; rounds: $ROUNDS.
+# Extra prof_run.py arguments: $PROF_ARGS; rounds: $ROUNDS; bench.py arguments: $BENCH_ARGS;
+# output directory name: $OUT (default: the mode).
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; cd "$R"
 MODE=${1:-iter}
-O="$R/gpurun_out/$MODE"; rm -rf "$O"; mkdir -p "$O"
+O="$R/gpurun_out/${OUT:-$MODE}"; rm -rf "$O"; mkdir -p "$O"
 step() { echo "== $*"; }
 tests() {
   timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TEST_ARGS} > "$O/gpu_tests.log" 2>&1

@@ -1,10 +1,11 @@
-"""Turn rocprofv3 --pmc passes into profiles/<round>/pmc_summary.json and profiles/pmc_traffic.json.
+"""Turn rocprofv3 --pmc passes into profiles/<round>/pmc_summary.json and profiles/pmc_traffic.json
+({workload: {kernel: HBM bytes per launch}}, read by bench.py for roofline.traffic).
 
 FETCH_SIZE/WRITE_SIZE are in KB per dispatch.  On gfx950 FETCH_SIZE under-reports wide
 coalesced reads by 2x (MI355X_MICROARCH.md §HBM); the factor actually applied is measured on
 tools/microbench/membench's copy kernel (known 159 MB read) and stored as fetch_correction.
 
-    python3 tools/make_pmc_traffic.py 'gpurun_out/r1/pmc_*' profiles/round1 "10000000 Imp3D push-sum" 'gpurun_out/r1/calib_*'
+    python3 tools/make_pmc_traffic.py 'gpurun_out/c3pmc/pmc_*' profiles/round2/c3 "10000000 Imp3D push-sum" [calib glob]
 """
 import csv
 import glob
@@ -44,7 +45,13 @@ out = {"workload": workload, "fetch_correction": corr, "calibration": calib_info
 os.makedirs(dst, exist_ok=True)
 with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
     json.dump(out, f, indent=1, sort_keys=True)
-traffic = {}
+path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+try:  # {workload: {kernel: entry}}: other workloads' entries are kept
+    traffic = json.load(open(path))
+    traffic = {w: e for w, e in traffic.items() if w != workload and isinstance(e, dict) and "workload" not in e}
+except (OSError, ValueError):
+    traffic = {}
+cur = traffic.setdefault(workload, {})
 for key, fetch in m.items():
     k, c = key.split("|")
     if c != "FETCH_SIZE":
@@ -53,9 +60,9 @@ for key, fetch in m.items():
     if w is None:
         continue
     short = k.split("::")[-1]
-    traffic[short] = {"workload": workload, "fetch_kb": fetch, "write_kb": w, "fetch_correction": corr,
-                      "hbm_bytes_per_launch": (fetch * corr + w) * 1024.0,
-                      "source": os.path.join(dst, "pmc_summary.json")}
-with open(os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_traffic.json"), "w") as f:
+    cur[short] = {"fetch_kb": fetch, "write_kb": w, "fetch_correction": corr,
+                  "hbm_bytes_per_launch": (fetch * corr + w) * 1024.0,
+                  "source": os.path.join(dst, "pmc_summary.json")}
+with open(path, "w") as f:
     json.dump(traffic, f, indent=1, sort_keys=True)
-print(json.dumps(traffic, indent=1))
+print(json.dumps(cur, indent=1))
