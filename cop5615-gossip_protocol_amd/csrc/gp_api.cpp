@@ -325,9 +325,7 @@ int build_links(Handle* h) {
         // per-slot link marks of the own slots (gossip chains, push-sum round tags)
         if ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))) return rc;
         // a remote sender's link message lands in the receiver's slot, read in CSR order (k_ps_pull<2>)
-        // (one GPU, kPushLink builds: every sender copies its link message into its slot)
-        const bool push = kPushLink && kFuseLinkMarks && !h->sharded && !h->gossip;
-        if (((h->sharded && h->world > 1) || push) && !h->gossip &&
+        if (h->sharded && h->world > 1 && !h->gossip &&
             ((rc = h->alloc(&h->rmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->rmsg[1], (size_t)nsl, slo))))
             return rc;
     }
@@ -436,8 +434,7 @@ bool fused_marks(const Handle* h) { return kFuseLinkMarks && !h->gossip && !h->g
 const char* round_kernel_name(const Handle* h) {
     if (h->gossip) return h->generic ? "k_gs_push" : (h->g.has_link ? "k_gs_pull<true>" : "k_gs_pull<false>");
     if (h->generic) return "k_ps_push_emit";
-    if (!h->g.has_link) return "k_ps_pull<0>";
-    return h->rmsg[0] ? (h->sharded ? "k_ps_pull<2>" : "k_ps_pull<3>") : "k_ps_pull<1>";
+    return h->g.has_link ? (h->rmsg[0] ? "k_ps_pull<2>" : "k_ps_pull<1>") : "k_ps_pull<0>";
 }
 
 const char* aux_kernel_name(const Handle* h) {

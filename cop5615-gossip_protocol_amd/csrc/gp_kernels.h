@@ -10,6 +10,11 @@ constexpr int kBlock = 256;       // 4 waves of 64
 #define GP_GRID_PER_CU 16
 #endif
 constexpr int kMaxGrid = 256 * GP_GRID_PER_CU;
+// Waves per SIMD the push-sum round kernel is compiled for (VGPR budget 512 / waves; A/B knob,
+// 7 ties, 8 spills and is 20% slower).
+#ifndef GP_PS_WAVES
+#define GP_PS_WAVES 6
+#endif
 constexpr int kParts = 64;          // completion sub-counters per round (one 64 B line each)
 constexpr int kPartStride = 16;     // u32 words between sub-counters
 constexpr int kPartRing = 4;        // rounds kept in the sub-counter ring
@@ -26,14 +31,6 @@ constexpr uint32_t kCtrStride = 32;  // u32 words between counters
 #define GP_FUSE_LINK 1
 #endif
 constexpr bool kFuseLinkMarks = GP_FUSE_LINK != 0;
-// Single-GPU Imp3D push-sum, with fused marks: the sender also copies its link message into its
-// CSR slot (rmsg, as a shard's exchange does for remote senders), so the receiver reads link
-// messages in slot order instead of gathering msg_prev[src].  1: slot messages read
-// unconditionally (one dependency level less); 2: only the marked ones.  A/B knob.
-#ifndef GP_PUSH_LINK
-#define GP_PUSH_LINK 0
-#endif
-constexpr int kPushLink = GP_PUSH_LINK;
 
 // Push-sum link-slot marks carry their round: the pass after F(r) writes link_tag(r) into the
 // CSR slot of every actor whose round-r message took its extra link, into the array of parity

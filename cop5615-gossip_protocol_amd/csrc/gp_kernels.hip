@@ -178,146 +178,133 @@ constexpr bool kNtStore16 = GP_NT16 != 0;
 // CSR slot of the first kLinkUnroll, the source id and link count (coalesced: CSR order);
 // (3) the messages of the links that fired.
 // LM: 0 no extra links; 1 links; 2 links on a shard of several ranks: a sender outside [lo, hi)
-// is remote, and the exchange wrote its message into the receiver's slot, rmsg_prev[slot];
-// 3 (kPushLink builds) one GPU, every link message read from the slot the sender copied it to.
-// Waves per SIMD the round kernel is compiled for (VGPR budget 512 / waves): the kernel is
-// latency-bound, so more resident waves = more loads in flight (A/B knob).
-#ifndef GP_PS_WAVES
-#define GP_PS_WAVES 6
-#endif
+// is remote, and the exchange wrote its message into the receiver's slot, rmsg_prev[slot].
 
+template <int LM>
+__device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v) {
+    const uint32_t m = presence(g, v);
+    if (!m) return 0;
+    const uint32_t code = (kAblate & 8u) ? kth_bit(m, v % popc(m))
+                                          : kth_bit(m, scale_draw(philox_x(v, r, kStreamPush, a.seed), popc(m)));
+    uint8_t f = a.flags[v];
+    double2 held = make_double2((double)v, 1.0);
+    double ss = 0.0, ww = 0.0;
+    uint32_t cin = 0;
+    if (r) {
+        held = a.msg_prev[v];
+        uint8_t d[6];
+#pragma unroll
+        for (uint32_t k = 0; k < 6; ++k) d[k] = load_sel(a.dir_prev, (m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
+        uint32_t li = 0, nl = 0;
+        if (LM) {
+            li = a.rev_off[v];
+            nl = (kAblate & 1u) ? 0u : a.rev_off[v + 1] - li;
+        }
+        uint32_t hits = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 6; ++k) hits |= ((m & slot_bit(k)) && d[k] == slot_code(k)) ? 1u << k : 0u;
+        if (kAblate & 16u) hits = 0;
+        uint32_t hk[3], rest = hits;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            hk[j] = rest ? (uint32_t)__builtin_ctz(rest) : 6u;
+            rest &= rest - 1u;
+        }
+        double2 gm[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) gm[j] = load_sel(a.msg_prev, hk[j] < 6u, slot_src(g, v, hk[j] < 6u ? hk[j] : 0u), v);
+        uint32_t gi = 0;
+        auto add = [&](double2 mm) {
+            ss += mm.x;
+            ww += mm.y;
+            ++cin;
+        };
+        auto flush = [&](uint32_t bound) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                if (gi == (uint32_t)j && hk[j] < 6u && slot_src(g, v, hk[j]) < bound) {
+                    add(gm[j]);
+                    ++gi;
+                }
+            if (gi >= 3) {
+                while (rest) {
+                    const uint32_t k = (uint32_t)__builtin_ctz(rest);
+                    const uint32_t u = slot_src(g, v, k);
+                    if (u >= bound) break;
+                    add(a.msg_prev[u]);
+                    rest &= rest - 1u;
+                }
+            }
+        };
+        if (LM) {
+            uint32_t ls[kLinkUnroll];
+#pragma unroll
+            for (uint32_t k = 0; k < kLinkUnroll; ++k) ls[k] = load_sel(a.rev_src, k < nl, li + k, a.slot_lo);
+            bool lk[kLinkUnroll];
+            double2 lm[kLinkUnroll];
+            uint8_t lc[kLinkUnroll];
+#pragma unroll
+            for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, a.slot_lo);
+            // ---- level 3: the messages of the sources whose slot is marked
+#pragma unroll
+            for (uint32_t k = 0; k < kLinkUnroll; ++k) {
+                lk[k] = k < nl && lc[k] == a.tag_prev;  // round-tagged marks: nothing to clear
+                if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
+                    lm[k] = a.rmsg_prev[li + k];
+                } else {
+                    lm[k] = load_sel(a.msg_prev, lk[k], ls[k], v);
+                }
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kLinkUnroll; ++k)
+                if (lk[k]) {
+                    flush(ls[k]);
+                    add(lm[k]);
+                }
+            for (uint32_t k = kLinkUnroll; k < nl; ++k) {  // rare: more than kLinkUnroll sources
+                if (a.lcnt_prev[li + k] == a.tag_prev) {
+                    const uint32_t u = a.rev_src[li + k];
+                    flush(u);
+                    add(LM == 2 && (u < a.lo || u >= a.hi) ? a.rmsg_prev[li + k] : a.msg_prev[u]);
+                }
+            }
+        }
+        flush(0xFFFFFFFFu);
+    }
+    const uint8_t f0 = f;
+    const PsOut o = ps_update(f, held, ss, ww, cin, a.delta, a.term_limit);
+    // non-temporal: the round's 160 MB of messages cannot stay in L2 until the next round
+    // reads them, and streaming them past it leaves L2 to the +-G, +-G^2 rows read now
+    // (measured ~1.5% per round; non-temporal LOADS of the CSR were 7% slower)
+    if (o.send) {
+        if constexpr (kNtStore16) {
+            nt_store16(&a.msg_cur[v], o.msg);
+        } else {
+            __builtin_nontemporal_store(o.msg.x, &a.msg_cur[v].x);
+            __builtin_nontemporal_store(o.msg.y, &a.msg_cur[v].y);
+        }
+    }
+    __builtin_nontemporal_store(o.send ? (uint8_t)code : kDirNone, &a.dir_cur[v]);
+    if constexpr (LM == 1 && kFuseLinkMarks) {  // the link pass's mark, written by the sender
+        if (o.send && code == kDirLink) a.lcnt_cur[a.lpos[v]] = (uint8_t)a.tag_cur;
+    }
+    if (f != f0) a.flags[v] = f;
+    if (o.conv_now) a.frozen[v] = o.msg;
+    return o.conv_now ? 1u : 0u;
+}
+
+// Grid-stride over the XCD-aware node range (a z-march walk, each workgroup carrying a tile up
+// through the planes so the +-G^2 rows come from L2, read 10% fewer lines but ran 12-20%
+// slower: DESIGN.md §8).
 template <int LM>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WAVES))) void k_ps_pull(RoundArgs a) {
     if (gate(a, a.r)) return;
     const Geom g = a.g;
     const uint32_t r = a.r;
+    uint32_t newly = 0;
     uint32_t v, end, step;
     node_range(a.lo, a.hi, a.span, v, end, step);
-    uint32_t newly = 0;
-    for (; v < end; v += step) {
-        const uint32_t m = presence(g, v);
-        if (m) {
-        const uint32_t code = (kAblate & 8u) ? kth_bit(m, v % popc(m))
-                                              : kth_bit(m, scale_draw(philox_x(v, r, kStreamPush, a.seed), popc(m)));
-        uint8_t f = a.flags[v];
-        double2 held = make_double2((double)v, 1.0);
-        double ss = 0.0, ww = 0.0;
-        uint32_t cin = 0;
-        if (r) {
-            held = a.msg_prev[v];
-            uint8_t d[6];
-#pragma unroll
-            for (uint32_t k = 0; k < 6; ++k) d[k] = load_sel(a.dir_prev, (m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
-            uint32_t li = 0, nl = 0;
-            if (LM) {
-                li = a.rev_off[v];
-                nl = (kAblate & 1u) ? 0u : a.rev_off[v + 1] - li;
-            }
-            uint32_t hits = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 6; ++k) hits |= ((m & slot_bit(k)) && d[k] == slot_code(k)) ? 1u << k : 0u;
-            if (kAblate & 16u) hits = 0;
-            uint32_t hk[3], rest = hits;
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                hk[j] = rest ? (uint32_t)__builtin_ctz(rest) : 6u;
-                rest &= rest - 1u;
-            }
-            double2 gm[3];
-#pragma unroll
-            for (int j = 0; j < 3; ++j) gm[j] = load_sel(a.msg_prev, hk[j] < 6u, slot_src(g, v, hk[j] < 6u ? hk[j] : 0u), v);
-            uint32_t gi = 0;
-            auto add = [&](double2 mm) {
-                ss += mm.x;
-                ww += mm.y;
-                ++cin;
-            };
-            auto flush = [&](uint32_t bound) {
-#pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    if (gi == (uint32_t)j && hk[j] < 6u && slot_src(g, v, hk[j]) < bound) {
-                        add(gm[j]);
-                        ++gi;
-                    }
-                if (gi >= 3) {
-                    while (rest) {
-                        const uint32_t k = (uint32_t)__builtin_ctz(rest);
-                        const uint32_t u = slot_src(g, v, k);
-                        if (u >= bound) break;
-                        add(a.msg_prev[u]);
-                        rest &= rest - 1u;
-                    }
-                }
-            };
-            if (LM) {
-                uint32_t ls[kLinkUnroll];
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k) ls[k] = load_sel(a.rev_src, k < nl, li + k, a.slot_lo);
-                bool lk[kLinkUnroll];
-                double2 lm[kLinkUnroll];
-                uint8_t lc[kLinkUnroll];
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, a.slot_lo);
-                if constexpr (LM == 3 && kPushLink == 1) {  // slot messages, same level as the marks
-#pragma unroll
-                    for (uint32_t k = 0; k < kLinkUnroll; ++k) lm[k] = load_sel(a.rmsg_prev, k < nl, li + k, a.slot_lo);
-                }
-                // ---- level 3: the messages of the sources whose slot is marked
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k) {
-                    lk[k] = k < nl && lc[k] == a.tag_prev;  // round-tagged marks: nothing to clear
-                    if constexpr (LM == 3) {
-                        if constexpr (kPushLink != 1) lm[k] = load_sel(a.rmsg_prev, lk[k], li + k, a.slot_lo);
-                    } else if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
-                        lm[k] = a.rmsg_prev[li + k];
-                    } else {
-                        lm[k] = load_sel(a.msg_prev, lk[k], ls[k], v);
-                    }
-                }
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k)
-                    if (lk[k]) {
-                        flush(ls[k]);
-                        add(lm[k]);
-                    }
-                for (uint32_t k = kLinkUnroll; k < nl; ++k) {  // rare: more than kLinkUnroll sources
-                    if (a.lcnt_prev[li + k] == a.tag_prev) {
-                        const uint32_t u = a.rev_src[li + k];
-                        flush(u);
-                        add(LM == 3 || (LM == 2 && (u < a.lo || u >= a.hi)) ? a.rmsg_prev[li + k] : a.msg_prev[u]);
-                    }
-                }
-            }
-            flush(0xFFFFFFFFu);
-        }
-        const uint8_t f0 = f;
-        const PsOut o = ps_update(f, held, ss, ww, cin, a.delta, a.term_limit);
-        // non-temporal: the round's 160 MB of messages cannot stay in L2 until the next round
-        // reads them, and streaming them past it leaves L2 to the +-G, +-G^2 rows read now
-        // (measured ~1.5% per round; non-temporal LOADS of the CSR were 7% slower)
-        if (o.send) {
-            if constexpr (kNtStore16) {
-                nt_store16(&a.msg_cur[v], o.msg);
-            } else {
-                __builtin_nontemporal_store(o.msg.x, &a.msg_cur[v].x);
-                __builtin_nontemporal_store(o.msg.y, &a.msg_cur[v].y);
-            }
-        }
-        __builtin_nontemporal_store(o.send ? (uint8_t)code : kDirNone, &a.dir_cur[v]);
-        if constexpr ((LM == 1 || LM == 3) && kFuseLinkMarks) {  // the link pass's mark, written by the sender
-            if (o.send && code == kDirLink) {
-                const uint32_t p = a.lpos[v];
-                a.lcnt_cur[p] = (uint8_t)a.tag_cur;
-                if constexpr (LM == 3) a.rmsg_cur[p] = o.msg;
-            }
-        }
-        if (f != f0) a.flags[v] = f;
-        if (o.conv_now) {
-            a.frozen[v] = o.msg;
-            ++newly;
-        }
-        }
-    }
+    for (; v < end; v += step) newly += ps_actor<LM>(a, g, r, v);
     block_add(newly, a.parts, r);
 }
 
@@ -1066,7 +1053,6 @@ uint32_t span_for(uint32_t n, int grid) {
 
 void launch_ps_pull(const RoundArgs& a, const Launch& l) {
     if (!a.g.has_link) hipLaunchKernelGGL(k_ps_pull<0>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
-    else if (a.rmsg_prev && !a.sharded) hipLaunchKernelGGL(k_ps_pull<3>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
     else if (a.rmsg_prev) hipLaunchKernelGGL(k_ps_pull<2>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
     else hipLaunchKernelGGL(k_ps_pull<1>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
 }
