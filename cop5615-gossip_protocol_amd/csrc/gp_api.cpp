@@ -449,8 +449,9 @@ const char* aux_kernel_name(const Handle* h) {
 //   push-sum pull: held (S,W) read 16 + message write 16 + flags read 1 + direction byte read
 //   1 (own row; neighbour rows re-read from cache) + direction write 1 per participant; Imp3D
 //   adds the link CSR offsets (4 per actor), per link the 4-byte source and 1-byte slot count,
-//   and the 16-byte message of every link that fired (~1 in 7: the interior degree).  The link
-//   count pass (a separate kernel) is not included.
+//   and the 16-byte message of every link that fired (~1 in 7: the interior degree); with the
+//   marks written by the round kernel (one GPU), each sender's 4-byte CSR slot and the 1-byte
+//   mark of every fired link.  A separate link count pass is not included.
 //   gossip pull: state byte read 1 + direction byte read 1 + write 1 (+ count r/w 8 on the
 //   receipts, not modelled); Imp3D adds offsets 4 per actor and 1 per link slot.
 double bytes_per_round(const Handle* h) {
@@ -463,6 +464,7 @@ double bytes_per_round(const Handle* h) {
     if (h->generic) return P * (16 + 16 + 16 + 1 + 4 + 4 + 4 + 4 + 4);
     double b = P * (16 + 16 + 1 + 1 + 1);
     if (h->g.has_link) b += 4 * A + links * (4 + 1) + links / 7 * 16;
+    if (fused_marks(h)) b += 4 * A + links / 7;
     return b;
 }
 

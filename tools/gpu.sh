@@ -5,6 +5,7 @@
 #   iter    tests + a bench line (no CPU baseline) + a kernel trace of 300 rounds (prof_run.py)
 #   bench   the default bench.py line (with the CPU baseline) + its rocprofv3 kernel trace/stats
 #   pmc     FETCH_SIZE and WRITE_SIZE passes (one run each) over 60 rounds of prof_run.py
+#   loop    kernel trace of W loopback shards of one graph (tools/shard_loopback_prof.py $LOOP_ARGS)
 #   ab      kernel-trace A/B of the variant libraries named in $VARIANTS (lib_<name>/, GP_LIB)
 # Extra prof_run.py arguments: $PROF_ARGS; rounds: $ROUNDS; bench.py arguments: $BENCH_ARGS;
 # output directory name: $OUT (default: the mode).
@@ -42,6 +43,8 @@ case $MODE in
       rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
     done
     python3 "$R/tools/pmc_summary.py" "$O" > "$O/summary.txt" 2>&1; cat "$O/summary.txt" ;;
+  loop)  # W shards of one graph on this GPU (loopback exchange) under a kernel trace
+    kt kt python3 "$R/tools/shard_loopback_prof.py" ${LOOP_ARGS} ;;
   ab)
     for v in ${VARIANTS}; do
       GP_LIB=lib_$v kt "kt_$v" python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-300} ${PROF_ARGS} || exit $?
