@@ -1,5 +1,9 @@
-# GPU suite on the current build, then the per-rank kernel costs of C5 (1e9-node Imp3D push-sum)
-# split over 8 shards on one GPU (loopback exchange), under a rocprofv3 kernel trace.
+# torch.distributed.run at world 1 with the shard engine (RCCL all-to-all of empty chunks):
+# C3 then C5, each under its own time limit, stage marks on stderr.
 set -o pipefail
-TEST_TIMEOUT=800 bash tools/gpu.sh tests || exit $?
-OUT=c5loop KT_TIMEOUT=500 KT_LINES=14 LOOP_ARGS="--world 8 --n 1000000000 --rounds 16" bash tools/gpu.sh loop
+mkdir -p gpurun_out/c5shard
+for w in c3 c5; do
+  timeout -k 10 150 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 \
+    bench.py --gpus 1 --engine shard --workload $w --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/c5shard/$w.json 2> gpurun_out/c5shard/$w.err
+  rc=$?; echo "$w rc=$rc"; grep "^\[bench" gpurun_out/c5shard/$w.err; grep "^{" gpurun_out/c5shard/$w.json | cut -c1-300; [ $rc -eq 0 ] || exit $rc
+done
