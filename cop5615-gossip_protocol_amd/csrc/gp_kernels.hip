@@ -148,7 +148,8 @@ constexpr uint32_t kLinkUnroll = GP_LINK_UNROLL;
 
 // Timing-only builds (tools/variants) may drop parts of the round kernel to price them; the
 // product is built with 0, and the results of any other value are wrong by construction.
-// bit 0: no extra-link collect; bit 3: no Philox draw; bit 4: no grid-hit messages.
+// bit 0: no extra-link collect; bit 3: no Philox draw; bit 4: no grid-hit messages; bit 5: full
+// gossip receipts as plain random stores instead of atomics.
 #ifndef GP_ABLATE
 #define GP_ABLATE 0
 #endif
@@ -763,8 +764,13 @@ __device__ __forceinline__ void gs_push_body(const RoundArgs& a, const Xchg* xp)
         if (!X) {
             if (tok) {
                 const uint4 px = philox(v, r, kStreamGossip, a.seed);
-                atomicAdd(&a.inc_cur[generic_target(a, v, m, scale_draw(px.x, d))], 1u);
-                if (tok > 1) atomicAdd(&a.inc_cur[generic_target(a, v, m, scale_draw(px.y, d))], 1u);
+                if constexpr (kAblate & 32u) {  // timing only: random plain stores for the atomics
+                    a.inc_cur[generic_target(a, v, m, scale_draw(px.x, d))] = 1u;
+                    if (tok > 1) a.inc_cur[generic_target(a, v, m, scale_draw(px.y, d))] = 1u;
+                } else {
+                    atomicAdd(&a.inc_cur[generic_target(a, v, m, scale_draw(px.x, d))], 1u);
+                    if (tok > 1) atomicAdd(&a.inc_cur[generic_target(a, v, m, scale_draw(px.y, d))], 1u);
+                }
             }
         } else {  // receipts for another rank's actors go to its send chunk (the target id)
             const Xchg& x = *xp;
