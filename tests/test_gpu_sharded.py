@@ -188,3 +188,27 @@ def test_shards_random_sweep(n, topo, algo, seed, world):
     _check_vs(ref, engines, algo)
     for e in engines:
         e.close()
+
+
+def test_shard_tables_scale_with_rank_count():
+    """Per-rank link tables: a rank holds the CSR of its own receivers and the
+    `lpos` of its own senders, not the global tables, so its device memory is its share of the
+    graph (+ two halo planes, the slot-indexed remote messages and the chunks), and the total
+    over 8 ranks stays within a small factor of one GPU's.  (Round 1 kept every global link
+    table on every rank: 16 B per global actor each.)"""
+    n = 8_000_000
+    one = Simulator(n, "Imp3D", "push-sum")
+    d1 = int(one.layout.device_bytes)
+    actors = one.actors
+    one.close()
+    ranks = [sharded.HipShard(n, "Imp3D", "push-sum", rank=r, world=8) for r in range(8)]
+    per = [int(e.layout.device_bytes) for e in ranks]
+    own = [e.hi - e.lo for e in ranks]
+    for e in ranks:
+        e.close()
+    for b, o in zip(per, own):
+        # own share of the single-GPU bytes, x2 for rmsg / halos / chunks, and far below a global
+        # table of 16 B per actor
+        assert b < 2.0 * d1 * o / actors, (b, d1, o, actors)
+        assert b < d1 / 2, (b, d1)
+    assert sum(per) < 2.0 * d1, (per, d1)
