@@ -1,15 +1,14 @@
-# A/B of the per-workgroup contiguous-run walk (GP_WALK) against the strided node-range walk:
-# headline convergence time through each build's CLI, C4 too, and read requests (PMC).
+# A/B of the wave-level gate overlapped with the first actor's loads (current tree, lib/) against
+# the barrier gate (lib_base, previous commit): C3, C2 line / 3D, C5w-sized Imp3D 100k; then the
+# GPU suite on the current tree.
 set -o pipefail
-V="base walk walkg6 walkg32"
 for i in 1 2 3; do
-  for v in $V; do
-    timeout -k 10 120 cop5615-gossip_protocol_amd/lib_$v/gossip 10000000 Imp3D push-sum > gpurun_out/cli_$v.$i.txt 2>&1 || exit $?
+  for v in base new; do
+    d=cop5615-gossip_protocol_amd/lib_$v; [ $v = new ] && d=cop5615-gossip_protocol_amd/lib
+    for w in "10000000 Imp3D push-sum" "100000 line push-sum" "100000 3D push-sum" "100000 Imp3D push-sum"; do
+      timeout -k 10 120 $d/gossip $w | grep Convergence | sed "s/^/$v $w: /" >> gpurun_out/gate_ab.txt || exit $?
+    done
   done
 done
-for v in $V; do timeout -k 10 120 cop5615-gossip_protocol_amd/lib_$v/gossip 100000000 full gossip > gpurun_out/cli4_$v.txt 2>&1 || exit $?; done
-for v in $V; do echo "$v $(grep -h Convergence gpurun_out/cli_$v.*.txt | sed 's/Convergence Time: //' | tr '\n' ' ') | c4 $(grep -h Convergence gpurun_out/cli4_$v.txt)"; done
-for v in base walk walkg6; do
-  GP_LIB=lib_$v OUT=wk_$v ROUNDS=60 PMC_EXTRA="TCC_EA0_RDREQ_sum,TCC_HIT_sum,TCC_MISS_sum" bash tools/gpu.sh pmc > gpurun_out/wk_$v.txt 2>&1 || exit $?
-  grep -E "k_ps_pull" gpurun_out/wk_$v/summary.txt | grep -E "RDREQ|HIT|MISS" | sed "s/^/$v /"
-done
+sort gpurun_out/gate_ab.txt
+TEST_TIMEOUT=800 bash tools/gpu.sh tests
