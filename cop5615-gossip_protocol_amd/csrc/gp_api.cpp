@@ -127,6 +127,7 @@ struct Handle {
     uint32_t* cnt = nullptr;
     uint8_t* gstate = nullptr;
     uint32_t* inc[2] = {nullptr, nullptr};
+    uint32_t* dbits = nullptr;  // full gossip on one GPU: done bitmap (k_gs_full4's sender filter)
     // generic push-sum buckets
     uint32_t* bcnt[2] = {nullptr, nullptr};
     uint32_t* boff[2] = {nullptr, nullptr};
@@ -229,6 +230,7 @@ struct Handle {
         a.frozen = frozen;
         a.cnt = cnt;
         a.gstate = gstate;
+        a.dbits = dbits;
         a.inc_prev = inc[p];
         a.inc_cur = inc[c];
         a.bcnt_prev = bcnt[p];
@@ -401,6 +403,7 @@ int reset(Handle* h) {
         if (h->generic) {
             HIP_TRY(hipMemsetAsync(h->inc[0] + lo, 0, n * sizeof(uint32_t), h->stream));
             HIP_TRY(hipMemsetAsync(h->inc[1] + lo, 0, n * sizeof(uint32_t), h->stream));
+            if (h->dbits) HIP_TRY(hipMemsetAsync(h->dbits, 0, (n + 31) / 32 * sizeof(uint32_t), h->stream));
         } else {
             launch_fill_u8(h->dir[0] + xlo, 0xFF, xn, h->stream);
             launch_fill_u8(h->dir[1] + xlo, 0xFF, xn, h->stream);
@@ -429,9 +432,13 @@ int reset(Handle* h) {
     return GP_OK;
 }
 
+// Full gossip on one GPU runs the four-actors-per-lane kernel with the done bitmap.
+bool full_quad(const Handle* h) { return h->gossip && h->full && !h->sharded && h->lo == 0; }
+
 bool fused_marks(const Handle* h) { return kFuseLinkMarks && !h->gossip && !h->generic && !h->sharded && h->g.has_link; }
 
 const char* round_kernel_name(const Handle* h) {
+    if (full_quad(h)) return "k_gs_full4";
     if (h->gossip) return h->generic ? "k_gs_push" : (h->g.has_link ? "k_gs_pull<true>" : "k_gs_pull<false>");
     if (h->generic) return "k_ps_push_emit";
     return h->g.has_link ? (h->rmsg[0] ? "k_ps_pull<2>" : "k_ps_pull<1>") : "k_ps_pull<0>";
@@ -485,6 +492,7 @@ void launch_main(Handle* h, int64_t k, const Xchg* x) {
     if (h->gossip) {
         if (h->generic) {  // adds into inc_cur, consumed (zeroed) by F(k+1)
             if (x) launch_gs_push_x(a, *x, l);
+            else if (full_quad(h)) launch_gs_full4(a, l);
             else launch_gs_push(a, l);
         } else {
             launch_gs_pull(a, l);
@@ -1018,6 +1026,7 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
         if ((rc = h->alloc(&h->cnt, n, lo)) || (rc = h->alloc(&h->gstate, n, lo))) return bail(rc);
         if (h->generic) {
             if ((rc = h->alloc(&h->inc[0], n, lo)) || (rc = h->alloc(&h->inc[1], n, lo))) return bail(rc);
+            if (full_quad(h) && (rc = h->alloc(&h->dbits, (n + 31) / 32))) return bail(rc);
         } else if ((rc = h->alloc(&h->dir[0], xn, xlo)) || (rc = h->alloc(&h->dir[1], xn, xlo))) {
             return bail(rc);
         }

@@ -86,6 +86,7 @@ struct RoundArgs {
     // gossip state
     uint32_t* cnt;            // messageCount (program.fs:75)
     uint8_t* gstate;          // tok (bits 0-1) | done (bit 2)
+    uint32_t* dbits;          // full gossip, one GPU: done bitmap (sender-side filter)
     uint32_t* inc_prev;       // generic path: receipts of round r-1 (atomics)
     uint32_t* inc_cur;
     // generic push-sum buckets (ping-pong)
@@ -169,6 +170,7 @@ void launch_link_count(const RoundArgs& a, const Launch& l);
 void launch_ps_push_emit(const RoundArgs& a, const Launch& l);
 void launch_ps_push_fill(const RoundArgs& a, uint32_t* slot_cur, const uint32_t* boff_cur, const Launch& l);
 void launch_gs_push(const RoundArgs& a, const Launch& l);
+void launch_gs_full4(const RoundArgs& a, const Launch& l);  // full gossip, one GPU (lo == 0)
 // sharded variants: remote link / full-topology messages go to the send chunks of x
 void launch_ps_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);
 void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);

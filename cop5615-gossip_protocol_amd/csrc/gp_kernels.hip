@@ -57,7 +57,7 @@ __device__ __forceinline__ void block_add(uint32_t c, uint32_t* parts, long long
 // it (one wave, 64 loads), so every block takes the same branch; block 0 publishes total[a-1]
 // and empties the ring slot that round a+2 will use.  Sharded: total[a-1] is the global count,
 // already written by the exchange's unpack (k_shard_unpack).
-__device__ __forceinline__ bool gate(const RoundArgs& A, long long a) {
+__device__ __forceinline__ unsigned long long gate_count(const RoundArgs& A, long long a) {
     __shared__ unsigned long long prev_s;
     if (threadIdx.x < 64) {
         if (A.sharded) {
@@ -76,8 +76,10 @@ __device__ __forceinline__ bool gate(const RoundArgs& A, long long a) {
         if (blockIdx.x == 0) *part_slot(A.parts, a + 2, threadIdx.x) = 0u;
     }
     __syncthreads();
-    return prev_s >= A.target;
+    return prev_s;
 }
+
+__device__ __forceinline__ bool gate(const RoundArgs& A, long long a) { return gate_count(A, a) >= A.target; }
 
 // program.fs:119-143 for one actor (round 0 = :110-116): absorb, test, halve, emit.
 // Returns the new message (s,w); sets conv_now when the actor converges this round.
@@ -813,6 +815,97 @@ __global__ __launch_bounds__(kBlock) void k_gs_push(RoundArgs a) { gs_push_body<
 
 __global__ __launch_bounds__(kBlock) void k_gs_push_x(RoundArgs a, Xchg x) { gs_push_body<true>(a, &x); }
 
+// Full-topology gossip on one GPU (program.fs:89-105, "full" neighbours program.fs:201-206):
+// four consecutive actors per lane, so the per-actor streams (state byte, receipt and count
+// words) are read as one dword / dwordx4 per lane.  Receipts are u32 atomics into inc_cur[t].
+// Sender-side done filter (program.fs:92): a sender skips a target whose bit in `dbits` is set.
+// A bit is set (atomicOr, once per actor) in the round its actor reports; done only ever turns
+// on, and the receiver applies the exact filter (state at round start) anyway, so a skipped
+// receipt is one the receiver would have dropped, and a stale 0 bit only costs an atomic.  The
+// filter is applied only once a quarter of the actors have reported (a bit read costs less than
+// the atomic it saves only when enough targets are done).
+__global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a) {
+    const uint32_t r = a.r;
+    unsigned long long prev = 0;
+    if (r) {
+        prev = gate_count(a, (long long)r - 1);
+        if (prev >= a.target) return;
+    }
+    const bool filter = 4ull * prev >= a.target;
+    const uint32_t na = a.hi;  // one GPU: actors [0, na)
+    const uint32_t nq = (na + 3u) >> 2;
+    const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;
+    uint32_t q, end, step;
+    node_range(0u, nq, span4, q, end, step);
+    uint32_t newly = 0;
+    // uniform per wave: the 8 lanes sharing a bitmap word reduce together
+    for (; q - (threadIdx.x & 63u) < end; q += step) {
+        const bool valid = q < end;
+        const uint32_t v0 = q << 2;
+        uint32_t st4 = 0, done4 = 0;
+        if (valid) {
+            st4 = *reinterpret_cast<const uint32_t*>(a.gstate + v0);
+            uint4 in4 = make_uint4(0u, 0u, 0u, 0u);
+            if (r) in4 = *reinterpret_cast<const uint4*>(a.inc_prev + v0);
+            uint32_t inc[4] = {in4.x, in4.y, in4.z, in4.w};
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                if (v0 + j >= na) inc[j] = 0u;  // the padding past the last actor
+            if (inc[0] | inc[1] | inc[2] | inc[3]) {
+                *reinterpret_cast<uint4*>(a.inc_prev + v0) = make_uint4(0u, 0u, 0u, 0u);
+                uint4 c4 = *reinterpret_cast<const uint4*>(a.cnt + v0);
+                uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
+                const uint32_t st0 = st4;
+                bool counted = false;
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t st = (st4 >> (8u * j)) & 0xFFu;
+                    uint32_t tok = st & 3u, done = (st >> 2) & 1u;
+                    if (inc[j] && !done) {
+                        counted = true;
+                        const uint32_t c0 = c[j], c1 = c0 + inc[j];
+                        c[j] = c1;
+                        if (c0 == 0) ++tok;                              // program.fs:99-100
+                        if (c0 <= a.threshold && c1 > a.threshold) {     // program.fs:102-104
+                            done = 1;
+                            ++newly;
+                            done4 |= 1u << j;
+                        }
+                        st4 = (st4 & ~(0xFFu << (8u * j))) | ((tok | (done << 2)) << (8u * j));
+                    }
+                }
+                if (counted) *reinterpret_cast<uint4*>(a.cnt + v0) = make_uint4(c[0], c[1], c[2], c[3]);
+                if (st4 != st0) *reinterpret_cast<uint32_t*>(a.gstate + v0) = st4;
+            }
+            // emit round r: one draw per activation chain (program.fs:89-95)
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t v = v0 + j, tok = (st4 >> (8u * j)) & 3u;
+                if (tok && v < na) {
+                    const uint4 px = philox(v, r, kStreamGossip, a.seed);
+                    const uint32_t t0 = scale_draw(px.x, a.nodes), u0 = t0 + (t0 >= v ? 1u : 0u);
+                    const uint32_t t1 = scale_draw(px.y, a.nodes), u1 = t1 + (t1 >= v ? 1u : 0u);
+                    const bool s1 = tok > 1;
+                    uint32_t b0 = 0, b1 = 0;
+                    if (filter) {
+                        b0 = a.dbits[u0 >> 5];
+                        if (s1) b1 = a.dbits[u1 >> 5];
+                    }
+                    if (!((b0 >> (u0 & 31u)) & 1u)) atomicAdd(&a.inc_cur[u0], 1u);
+                    if (s1 && !((b1 >> (u1 & 31u)) & 1u)) atomicAdd(&a.inc_cur[u1], 1u);
+                }
+            }
+        }
+        // the reports of this round into the done bitmap: 8 lanes = 32 actors = one word
+        uint32_t w = done4 << ((q & 7u) * 4u);
+        w |= __shfl_xor(w, 1, 64);
+        w |= __shfl_xor(w, 2, 64);
+        w |= __shfl_xor(w, 4, 64);
+        if (w && (q & 7u) == 0u) atomicOr(&a.dbits[q >> 3], w);
+    }
+    if (r) block_add(newly, a.parts, (long long)r - 1);
+}
+
 // Push-sum on any topology (used for "full"): messages are bucketed by destination with an
 // integer atomic (slot order is arbitrary), then each receiver visits its bucket in ascending
 // source order (selection by repeated minimum; buckets hold ~1 entry), so the fp64 sum is the
@@ -1091,6 +1184,10 @@ void launch_ps_push_emit(const RoundArgs& a, const Launch& l) {
 
 void launch_ps_push_fill(const RoundArgs& a, uint32_t* slot_cur, const uint32_t* boff_cur, const Launch& l) {
     hipLaunchKernelGGL(k_ps_push_fill, dim3(l.grid), dim3(kBlock), 0, l.stream, a, slot_cur, boff_cur);
+}
+
+void launch_gs_full4(const RoundArgs& a, const Launch& l) {
+    hipLaunchKernelGGL(k_gs_full4, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
 }
 
 void launch_gs_push(const RoundArgs& a, const Launch& l) {

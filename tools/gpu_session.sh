@@ -1,12 +1,13 @@
-# A/B of the full-gossip sender-side done filter (lib_gsf = this tree) against lib_base (previous
-# commit): GPU suite on this tree, then CLI convergence times and a kernel trace of C4.
+# Full gossip: four actors per lane + done bitmap (lib/, this tree) against the per-actor kernel
+# with the gstate sender filter (lib_base): GPU suite, CLI times, C4 bench + kernel trace.
 set -o pipefail
 O=gpurun_out/ab; rm -rf $O; mkdir -p $O
 TEST_TIMEOUT=800 bash tools/gpu.sh tests || exit $?
 for i in 1 2 3; do
-  for v in base gsf; do
+  for v in base ""; do
+    d=cop5615-gossip_protocol_amd/lib${v:+_$v}
     for w in "100000000 full gossip" "10000000 full gossip" "1000 full gossip"; do
-      timeout -k 10 120 cop5615-gossip_protocol_amd/lib_$v/gossip $w | grep Convergence | sed "s/^/$v $w: /" >> $O/cli.txt || exit $?
+      timeout -k 10 120 $d/gossip $w | grep Convergence | sed "s/^/${v:-new} $w: /" >> $O/cli.txt || exit $?
     done
   done
 done
