@@ -822,8 +822,11 @@ __global__ __launch_bounds__(kBlock) void k_gs_push_x(RoundArgs a, Xchg x) { gs_
 // A bit is set (atomicOr, once per actor) in the round its actor reports; done only ever turns
 // on, and the receiver applies the exact filter (state at round start) anyway, so a skipped
 // receipt is one the receiver would have dropped, and a stale 0 bit only costs an atomic.  The
-// filter is applied only once a quarter of the actors have reported (a bit read costs less than
-// the atomic it saves only when enough targets are done).
+// filter is applied only once 1/GP_GS_FILTER_DIV of the actors have reported (a bit read costs
+// less than the atomic it saves only when enough targets are done).
+#ifndef GP_GS_FILTER_DIV
+#define GP_GS_FILTER_DIV 16
+#endif
 __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a) {
     const uint32_t r = a.r;
     unsigned long long prev = 0;
@@ -831,7 +834,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a) {
         prev = gate_count(a, (long long)r - 1);
         if (prev >= a.target) return;
     }
-    const bool filter = 4ull * prev >= a.target;
+    const bool filter = (unsigned long long)GP_GS_FILTER_DIV * prev >= a.target;
     const uint32_t na = a.hi;  // one GPU: actors [0, na)
     const uint32_t nq = (na + 3u) >> 2;
     const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;

@@ -1,15 +1,12 @@
-# Full gossip: four actors per lane + done bitmap (lib/, this tree) against the per-actor kernel
-# with the gstate sender filter (lib_base): GPU suite, CLI times, C4 bench + kernel trace.
+# k_gs_full4 filter threshold A/B: the done-bitmap filter from the first report (f1), from 1/64,
+# 1/16, 1/4 (f4 = default) of the actors reported.
 set -o pipefail
 O=gpurun_out/ab; rm -rf $O; mkdir -p $O
-TEST_TIMEOUT=800 bash tools/gpu.sh tests || exit $?
 for i in 1 2 3; do
-  for v in base ""; do
-    d=cop5615-gossip_protocol_amd/lib${v:+_$v}
-    for w in "100000000 full gossip" "10000000 full gossip" "1000 full gossip"; do
-      timeout -k 10 120 $d/gossip $w | grep Convergence | sed "s/^/${v:-new} $w: /" >> $O/cli.txt || exit $?
+  for v in f4 f1 f16 f64; do
+    for w in "100000000 full gossip" "10000000 full gossip"; do
+      timeout -k 10 120 cop5615-gossip_protocol_amd/lib_$v/gossip $w | grep Convergence | sed "s/^/$v $w: /" >> $O/cli.txt || exit $?
     done
   done
 done
 sort $O/cli.txt
-OUT=c4 BENCH_ARGS="--workload c4 --steps 3" bash tools/gpu.sh bench
