@@ -152,6 +152,20 @@ def roofline(ks, bytes_per_update, actors, wl):
             "layout_frac": round(ks["bytes_per_launch"] / (ks["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+def strong_scaling_base(name):
+    """The one-GPU point of the strong-scaling curve of workload `name` (N > 1 runs split one
+    graph): the committed N = 1 bench line of the same workload, so a reader can form the
+    efficiency against the same graph (the driver's N = 1 run is the c3 headline)."""
+    path = os.path.join(ROOT, "profiles", "round2", name, "bench_line_n1.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return {"value": d["value"], "unit": d["unit"], "workload": d["config"]["workload"],
+                "source": os.path.relpath(path, ROOT)}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def progress(rank, msg, t0=time.perf_counter()):
     """Rank 0 stage marks on stderr (stdout carries only the JSON line)."""
     if rank == 0:
@@ -272,6 +286,8 @@ def main():
         }
         if per_rank:
             out["per_rank"] = per_rank
+        if world > 1:
+            out["strong_scaling_base"] = strong_scaling_base(name)
         print(json.dumps(out), flush=True)
     eng.close()
     if use_shards:

@@ -1,12 +1,9 @@
-# k_gs_full4 filter threshold A/B: the done-bitmap filter from the first report (f1), from 1/64,
-# 1/16, 1/4 (f4 = default) of the actors reported.
+# Refresh of this round's measurements on the final kernels: GPU suite, C3 bench line (CPU
+# baseline) + kernel trace, C4 PMC (active-round means), C5 one-GPU line.
 set -o pipefail
-O=gpurun_out/ab; rm -rf $O; mkdir -p $O
-for i in 1 2 3; do
-  for v in f4 f1 f16 f64; do
-    for w in "100000000 full gossip" "10000000 full gossip"; do
-      timeout -k 10 120 cop5615-gossip_protocol_amd/lib_$v/gossip $w | grep Convergence | sed "s/^/$v $w: /" >> $O/cli.txt || exit $?
-    done
-  done
-done
-sort $O/cli.txt
+TEST_TIMEOUT=800 bash tools/gpu.sh tests || exit $?
+OUT=c3 bash tools/gpu.sh bench || exit $?
+OUT=c4pmc ROUNDS=75 PROF_ARGS="--n 100000000 --topology full --algorithm gossip" PMC_EXTRA="TCC_EA0_ATOMIC_sum,TCC_EA0_WRREQ_sum" bash tools/gpu.sh pmc || exit $?
+mkdir -p gpurun_out/c5
+timeout -k 10 400 python3 bench.py --workload c5 --steps 2 > gpurun_out/c5/bench.json 2> gpurun_out/c5/bench.err
+rc=$?; echo "c5 rc=$rc"; cat gpurun_out/c5/bench.json; exit $rc

@@ -6,6 +6,12 @@ coalesced reads by 2x (MI355X_MICROARCH.md §HBM); the factor actually applied i
 tools/microbench/membench's copy kernel (known 159 MB read) and stored as fetch_correction.
 
     python3 tools/make_pmc_traffic.py 'gpurun_out/c3pmc/pmc_*' profiles/round2/c3 "10000000 Imp3D push-sum" [calib glob]
+
+PMC_STAT=active_mean: per (kernel, counter) the mean over the dispatches whose value is at least
+1% of that counter's largest dispatch (the rounds that ran, not the gated-off launches past
+convergence) instead of the median over all dispatches: for workloads whose rounds differ a lot
+(C4 full gossip: 0.08 to 4.4 ms per round), so the figure matches the mean kernel time bench.py
+divides by.
 """
 import csv
 import glob
@@ -27,11 +33,20 @@ def medians(root, skip_first=1):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
             agg[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
+    if os.environ.get("PMC_STAT") == "active_mean":
+        out = {}
+        for (k, c), v in agg.items():
+            top = max(v) if v else 0.0
+            act = [x for x in v if x >= 0.01 * top] or v
+            out[f"{k}|{c}"] = statistics.fmean(act)
+        return out
     return {f"{k}|{c}": statistics.median(v[skip_first:] or v) for (k, c), v in agg.items()}
 
 
 m = medians(src)
-corr = 2.0
+# PMC_FETCH_CORR: the FETCH_SIZE factor when no calibration run is given (2 for wide coalesced
+# streaming reads, MI355X_MICROARCH.md; random narrow reads are uncalibrated: 1 = lower bound)
+corr = float(os.environ.get("PMC_FETCH_CORR", "2.0"))
 calib_info = None
 if calib:
     cm = medians(calib, skip_first=0)
@@ -41,7 +56,8 @@ if calib:
         corr = known / fetch[0]
         calib_info = {"kernel": "membench copy_flat (16 B/lane coalesced read)", "fetch_kb": fetch[0],
                       "known_kb": known, "factor": corr}
-out = {"workload": workload, "fetch_correction": corr, "calibration": calib_info, "medians": m}
+out = {"workload": workload, "fetch_correction": corr, "calibration": calib_info,
+       "statistic": os.environ.get("PMC_STAT", "median"), "medians": m}
 os.makedirs(dst, exist_ok=True)
 with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
     json.dump(out, f, indent=1, sort_keys=True)
