@@ -71,3 +71,36 @@ def test_async_is_seed_deterministic():
     b, y = oracle.async_run(100, "Imp3D", "push-sum", seed=7)
     assert (a.steps, a.completed) == (b.steps, b.completed)
     np.testing.assert_array_equal(x["S"].view(np.uint64), y["S"].view(np.uint64))
+
+
+# ---- report.pdf p.4-5 sweeps ("compare distributions against the report.pdf
+# p.4-5 sweeps").  Cost of a run in each model: the async model's processed messages and the
+# round mode's node-updates (actors x rounds), each averaged over three seeds; both must rise
+# with N the way the report's wall times do (rank correlation over N = 20 ... 1000).
+from report_sweeps import MIN_RHO, REPORT_MS, SWEEP_N, spearman  # noqa: E402
+
+
+@pytest.mark.parametrize("algo,topo", sorted(REPORT_MS))
+def test_cost_over_n_follows_report_sweep(algo, topo):
+    ms, asy, rnd = [], [], []
+    for n, t in zip(SWEEP_N, REPORT_MS[(algo, topo)]):
+        if t is None:
+            continue
+        a, r = [], []
+        for s in SEEDS:
+            st, _ = oracle.async_run(n, topo, algo, seed=s, max_steps=20_000_000)
+            if st.converged:
+                a.append(float(st.messages))
+            sim = oracle.OracleSim(n, topo, algo, seed=s)
+            rs = sim.step(1 << 22)
+            assert rs.converged
+            r.append(float(sim.actors) * int(rs.round))
+            sim.close()
+        if a:  # the async line / 2D push-sum runs at the top sizes may outlast the step cap
+            ms.append(t)
+            asy.append(np.mean(a))
+            rnd.append(np.mean(r))
+    assert len(ms) >= 8, (algo, topo, len(ms))
+    rho_async, rho_round = spearman(ms, asy), spearman(ms, rnd)
+    assert rho_async >= MIN_RHO[(algo, topo)], (algo, topo, rho_async, ms, asy)
+    assert rho_round >= MIN_RHO[(algo, topo)], (algo, topo, rho_round, ms, rnd)

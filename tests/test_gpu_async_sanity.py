@@ -95,3 +95,27 @@ def test_topology_cost_ranking_agrees_with_async(algo):
         rounds[t], steps[t] = np.mean(r), np.mean(q)
     for cost in (rounds, steps):
         assert min(cost["line"], cost["2D"]) > 2.0 * max(cost["full"], cost["Imp3D"]), (rounds, steps)
+
+
+# The HIP round engine's cost (node-updates to convergence, three seeds) over report.pdf's
+# sweep sizes rises with N the way the reference's published wall times do (tests/report_sweeps.py).
+from report_sweeps import MIN_RHO, REPORT_MS, SWEEP_N, spearman  # noqa: E402
+
+
+@pytest.mark.parametrize("algo,topo", sorted(REPORT_MS))
+def test_engine_cost_over_n_follows_report_sweep(algo, topo):
+    ms, cost = [], []
+    for n, t in zip(SWEEP_N, REPORT_MS[(algo, topo)]):
+        if t is None:
+            continue
+        c = []
+        for s in (1, 2, 3):
+            sim = Simulator(n, topo, algo, seed=s)
+            st = sim.step(1 << 22)
+            assert st.converged
+            c.append(float(sim.actors) * int(st.round))
+            sim.close()
+        ms.append(t)
+        cost.append(np.mean(c))
+    rho = spearman(ms, cost)
+    assert rho >= MIN_RHO[(algo, topo)], (algo, topo, rho, ms, cost)
