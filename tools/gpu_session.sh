@@ -1,9 +1,10 @@
-# Refresh of this round's measurements on the final kernels: GPU suite, C3 bench line (CPU
-# baseline) + kernel trace, C4 PMC (active-round means), C5 one-GPU line.
+# A/B repeat: contiguous >= 1 GiB allocations at 1e9 actors (30 rounds each, alternating).
 set -o pipefail
-TEST_TIMEOUT=800 bash tools/gpu.sh tests || exit $?
-OUT=c3 bash tools/gpu.sh bench || exit $?
-OUT=c4pmc ROUNDS=75 PROF_ARGS="--n 100000000 --topology full --algorithm gossip" PMC_EXTRA="TCC_EA0_ATOMIC_sum,TCC_EA0_WRREQ_sum" bash tools/gpu.sh pmc || exit $?
-mkdir -p gpurun_out/c5
-timeout -k 10 400 python3 bench.py --workload c5 --steps 2 > gpurun_out/c5/bench.json 2> gpurun_out/c5/bench.err
-rc=$?; echo "c5 rc=$rc"; cat gpurun_out/c5/bench.json; exit $rc
+O=$GRAFT_REPO_ROOT/gpurun_out/contig2; rm -rf $O; mkdir -p $O
+for i in 1 2 3; do
+  for v in base contig; do
+    GP_LIB=lib_$v timeout -k 10 300 python3 tools/prof_run.py --n 1000000000 --rounds 30 2>/dev/null | sed "s/^/$v: /" >> $O/runs.txt
+    rc=$?; [ $rc -eq 0 ] || exit $rc
+  done
+done
+sort $O/runs.txt
