@@ -194,7 +194,10 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
     double ss = 0.0, ww = 0.0;
     uint32_t cin = 0;
     if (r) {
-        held = a.msg_prev[v];
+#ifndef GP_SKIP_CONV_HELD
+#define GP_SKIP_CONV_HELD 1
+#endif
+        if (!GP_SKIP_CONV_HELD) held = a.msg_prev[v];
         uint8_t d[6];
 #pragma unroll
         for (uint32_t k = 0; k < 6; ++k) d[k] = load_sel(a.dir_prev, (m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
@@ -216,6 +219,10 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
         double2 gm[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) gm[j] = load_sel(a.msg_prev, hk[j] < 6u, slot_src(g, v, hk[j] < 6u ? hk[j] : 0u), v);
+        // A converged actor only relays what arrives (program.fs:125-127): its held (S,W) and so
+        // its message row are not read (more than half of the C3 run's actor-rounds).  Issued
+        // with the second load level, when the flags byte has long arrived.
+        if (GP_SKIP_CONV_HELD && !(f & 16u)) held = a.msg_prev[v];
         uint32_t gi = 0;
         auto add = [&](double2 mm) {
             ss += mm.x;
