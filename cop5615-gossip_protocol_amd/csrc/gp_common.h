@@ -130,9 +130,11 @@ __host__ __device__ __forceinline__ uint32_t presence(const Geom& g, uint32_t v)
     return m;
 }
 
-// Index of the k-th set bit of m (k < popcount(m)).
+// Index of the k-th set bit of m (k < popcount(m) <= 7: six grid directions + the extra link).
+// Six predicated steps instead of a k-trip loop: no divergent branch in a wave.
 __host__ __device__ __forceinline__ uint32_t kth_bit(uint32_t m, uint32_t k) {
-    for (uint32_t i = 0; i < k; ++i) m &= m - 1u;
+#pragma unroll
+    for (uint32_t i = 0; i < 6; ++i) m = i < k ? (m & (m - 1u)) : m;
 #if defined(__HIP_DEVICE_COMPILE__)
     return (uint32_t)__builtin_ctz(m);
 #else
