@@ -119,15 +119,13 @@ __device__ __forceinline__ PsOut ps_update(uint8_t& f, double2 held, double ss, 
 // Grid in-neighbour slots in ascending source order: v-P, v-G, v-1, v+1, v+G, v+P (presence
 // bits 4, 2, 0, 1, 3, 5); the sender in slot k targets v iff its direction code is the
 // opposite one (5, 3, 1, 0, 2, 4).
+// (Bit masks, not a switch or a select chain: with a run-time k those compile to a divergent
+// branch tree.)
 __device__ __forceinline__ uint32_t slot_src(const Geom& g, uint32_t v, uint32_t k) {
-    switch (k) {
-    case 0: return v - g.plane;
-    case 1: return v - g.gx;
-    case 2: return v - 1u;
-    case 3: return v + 1u;
-    case 4: return v + g.gx;
-    default: return v + g.plane;
-    }
+    const uint32_t kk = k < 3u ? k : 5u - k;  // 0: +-G^2, 1: +-G, 2: +-1
+    const uint32_t mag = (g.plane & (0u - (uint32_t)(kk == 0u))) | (g.gx & (0u - (uint32_t)(kk == 1u))) |
+                         (uint32_t)(kk == 2u);
+    return k < 3u ? v - mag : v + mag;
 }
 
 // Slot k of v exists iff presence bit kSlotBit(k) is set; its sender targets v iff its
@@ -215,7 +213,7 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
         uint32_t gs[3], rest = hits;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            gs[j] = rest ? slot_src(g, v, (uint32_t)__builtin_ctz(rest)) : 0xFFFFFFFFu;
+            gs[j] = slot_src(g, v, (uint32_t)__builtin_ctz(rest | 64u)) | (0u - (uint32_t)(rest == 0u));
             rest &= rest - 1u;
         }
         double2 gm[3];

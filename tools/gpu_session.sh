@@ -1,10 +1,10 @@
-# A/B of the merge (ordered fp64 inbox sum): lib_base (HEAD), p0 (grid-hit sources computed
-# once, branchy merge), q (p0 + grid-hit sources reused as load addresses, branch-free kth_bit); GPU suite on q (= lib/).
+# A/B: branch-free (mask) slot_src and grid-hit sources (lib_s = this tree) vs HEAD (lib_base);
+# GPU suite on this tree.
 set -o pipefail
 O=$GRAFT_REPO_ROOT/gpurun_out/merge; rm -rf $O; mkdir -p $O
 TEST_TIMEOUT=800 bash tools/gpu.sh tests || exit $?
 for i in 1 2 3; do
-  for v in base p0 q; do
+  for v in base s; do
     for w in "10000000 Imp3D push-sum" "100000000 Imp3D push-sum" "100000 3D push-sum"; do
       timeout -k 10 120 cop5615-gossip_protocol_amd/lib_$v/gossip $w | grep Convergence | sed "s/^/$v $w: /" >> $O/cli.txt || exit $?
     done
