@@ -6,6 +6,14 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+// Quiet-wave skipping of the push-sum round kernel (one GPU, from kQuietMinActors actors or under
+// GP_FLAG_QUIET_WAVES): the marks are kept once this percentage of the nodes has converged (0:
+// off; A/B knob).  On small graphs the round is latency-bound and the marks only add work.
+#ifndef GP_ACT_PCT
+#define GP_ACT_PCT 99
+#endif
+constexpr uint32_t kQuietMinActors = 1u << 20;
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -123,6 +131,8 @@ struct Handle {
     uint8_t* dir[2] = {nullptr, nullptr};
     uint8_t* flags = nullptr;
     double2* frozen = nullptr;
+    uint8_t* act[2] = {nullptr, nullptr};  // quiet-wave marks, one byte per 64 actors (ping-pong)
+    uint32_t act_thr = 0;
     // gossip
     uint32_t* cnt = nullptr;
     uint8_t* gstate = nullptr;
@@ -209,7 +219,8 @@ struct Handle {
         a.full = full ? 1u : 0u;
         a.nodes = (uint32_t)lay.nodes;
         a.span = span;
-        a.threshold = (uint32_t)cfg.gossip_threshold;
+        if (gossip) a.threshold = (uint32_t)cfg.gossip_threshold;
+        else a.act_thr = act_thr;
         a.delta = cfg.delta;
         a.term_limit = (uint32_t)cfg.term_limit;
         a.total = total;
@@ -228,8 +239,13 @@ struct Handle {
         a.dir_cur = dir[c];
         a.flags = flags;
         a.frozen = frozen;
-        a.cnt = cnt;
-        a.gstate = gstate;
+        if (gossip) {
+            a.cnt = cnt;
+            a.gstate = gstate;
+        } else {
+            a.act_prev = act[r & 1u];
+            a.act_cur = act[(r + 1u) & 1u];
+        }
         a.dbits = dbits;
         a.inc_prev = inc[p];
         a.inc_cur = inc[c];
@@ -371,6 +387,9 @@ int ensure_trace(Handle* h, int64_t need) {
     return GP_OK;
 }
 
+// Quiet-wave marks: one byte per 64 actors.
+size_t act_bytes(const Handle* h) { return (size_t)(h->g.actors + 63u) / 64u + 1u; }
+
 int reset(Handle* h) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     const size_t lo = h->lo, n = h->own();
@@ -396,6 +415,8 @@ int reset(Handle* h) {
         } else {
             launch_fill_u8(h->dir[0] + xlo, kDirNone, xn, h->stream);
             launch_fill_u8(h->dir[1] + xlo, kDirNone, xn, h->stream);
+            for (uint8_t* q : h->act)
+                if (q) HIP_TRY(hipMemsetAsync(q, 0, act_bytes(h), h->stream));
         }
     } else {
         HIP_TRY(hipMemsetAsync(h->cnt + lo, 0, n * sizeof(uint32_t), h->stream));
@@ -441,7 +462,8 @@ const char* round_kernel_name(const Handle* h) {
     if (full_quad(h)) return "k_gs_full4";
     if (h->gossip) return h->generic ? "k_gs_push" : (h->g.has_link ? "k_gs_pull<true>" : "k_gs_pull<false>");
     if (h->generic) return "k_ps_push_emit";
-    return h->g.has_link ? (h->rmsg[0] ? "k_ps_pull<2>" : "k_ps_pull<1>") : "k_ps_pull<0>";
+    if (h->g.has_link) return h->rmsg[0] ? "k_ps_pull<2, false>" : h->act[0] ? "k_ps_pull<1, true>" : "k_ps_pull<1, false>";
+    return h->act[0] ? "k_ps_pull<0, true>" : "k_ps_pull<0, false>";
 }
 
 const char* aux_kernel_name(const Handle* h) {
@@ -538,10 +560,19 @@ int ensure_events(Handle* h, int64_t rounds) {
     return GP_OK;
 }
 
+// Quiet-wave marks for round k + 1 go into act[(k + 1) & 1] during F(k), tagged link_tag(k + 1):
+// clear that array before a tag value repeats in it (after F(k - 1) has read it).
+int clear_act_if_due(Handle* h, int64_t k) {
+    if (!h->act[0] || !tag_clear_round((uint32_t)(k + 1))) return GP_OK;
+    HIP_TRY(hipMemsetAsync(h->act[(k + 1) & 1], 0, act_bytes(h), h->stream));
+    return GP_OK;
+}
+
 // Round k with its three timing events (slot i of the event ring).
 int launch_round(Handle* h, int64_t k, const Xchg* x, bool timing, int64_t i) {
     int rc;
     if (fused_marks(h) && (rc = clear_tags_if_due(h, (uint32_t)k))) return rc;
+    if ((rc = clear_act_if_due(h, k))) return rc;
     if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i], h->stream));
     launch_main(h, k, x);
     if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i + 1], h->stream));
@@ -1037,6 +1068,12 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
             (rc = h->alloc(&h->flags, n, lo)) || (rc = h->alloc(&h->frozen, n, lo)) ||
             (rc = h->alloc(&h->partials, (size_t)h->grid)))
             return bail(rc);
+        if (GP_ACT_PCT > 0 && !h->generic && !h->sharded &&
+            (h->g.actors >= kQuietMinActors || (cfg->flags & GP_FLAG_QUIET_WAVES))) {  // quiet-wave marks
+            for (int i = 0; i < 2; ++i)
+                if ((rc = h->alloc(&h->act[i], act_bytes(h)))) return bail(rc);
+            h->act_thr = (uint32_t)((uint64_t)h->lay.nodes * GP_ACT_PCT / 100u);
+        }
         if (h->generic) {  // single-GPU only: whole graph
             for (int i = 0; i < 2; ++i)
                 if ((rc = h->alloc(&h->bcnt[i], A)) || (rc = h->alloc(&h->boff[i], A + 1)) ||

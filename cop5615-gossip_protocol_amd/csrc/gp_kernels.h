@@ -57,7 +57,10 @@ struct RoundArgs {
     uint32_t full;         // full topology (implicit k + (k >= v) neighbour map)
     uint32_t nodes;        // `nodes` (full topology degree)
     uint32_t span;         // per-XCD contiguous node range (XCD-aware block mapping)
-    uint32_t threshold;    // gossip report threshold (program.fs:102)
+    union {  // gossip | push-sum (a handle runs one algorithm; the kernel arguments stay small)
+        uint32_t threshold;  // gossip report threshold (program.fs:102)
+        uint32_t act_thr;    // quiet-wave marks kept from this many converged actors (below)
+    };
     double delta;          // push-sum delta (program.fs:187)
     uint32_t term_limit;   // program.fs:135
     uint32_t ps_tags;      // push-sum: link marks are round tags (link_tag); gossip: chain counts
@@ -84,8 +87,20 @@ struct RoundArgs {
     uint8_t* flags;           // termRound (bits 0-3) | converged (bit 4)
     double2* frozen;          // (S,W) frozen at convergence (program.fs:125-127)
     // gossip state
-    uint32_t* cnt;            // messageCount (program.fs:75)
-    uint8_t* gstate;          // tok (bits 0-1) | done (bit 2)
+    union {
+        struct {  // gossip state
+            uint32_t* cnt;     // messageCount (program.fs:75)
+            uint8_t* gstate;   // tok (bits 0-1) | done (bit 2)
+        };
+        // Quiet-wave skipping (one GPU, push-sum): act_cur[w] = link_tag(r + 1) when the 64 actors
+        // of wave w may have work in round r + 1 (one of them has not converged, or a round-r
+        // message targets one of them); written by F(r) once act_thr actors have converged, read
+        // by F(r + 1).
+        struct {
+            const uint8_t* act_prev;  // marks for this round (written by F(r - 1)); null: off
+            uint8_t* act_cur;
+        };
+    };
     uint32_t* dbits;          // full gossip, one GPU: done bitmap (sender-side filter)
     uint32_t* inc_prev;       // generic path: receipts of round r-1 (atomics)
     uint32_t* inc_cur;

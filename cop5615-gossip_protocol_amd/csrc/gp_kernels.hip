@@ -182,7 +182,8 @@ constexpr bool kNtStore16 = GP_NT16 != 0;
 // is remote, and the exchange wrote its message into the receiver's slot, rmsg_prev[slot].
 
 template <int LM>
-__device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v) {
+__device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
+                                             bool mark = false) {
     const uint32_t m = presence(g, v);
     if (!m) return 0;
     const uint32_t code = (kAblate & 8u) ? kth_bit(m, v % popc(m))
@@ -302,21 +303,40 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
     }
     if (f != f0) a.flags[v] = f;
     if (o.conv_now) a.frozen[v] = o.msg;
+    if (mark) {  // the waves with work in round r + 1: v's own if it still updates, its target's
+        const uint8_t t = (uint8_t)link_tag(r + 1u);
+        if (!(f & 16u)) a.act_cur[v >> 6] = t;
+        if (o.send) a.act_cur[dir_target(g, v, code, code == kDirLink ? link_of(a.seed, v, a.nodes) : 0u) >> 6] = t;
+    }
     return o.conv_now ? 1u : 0u;
 }
 
 // Grid-stride over the XCD-aware node range (a z-march walk, each workgroup carrying a tile up
 // through the planes so the +-G^2 rows come from L2, read 10% fewer lines but ran 12-20%
 // slower: DESIGN.md §8).
-template <int LM>
+// Quiet waves (one GPU, once act_thr actors have converged): a wave of 64 actors that F(r - 1)
+// did not mark has only converged actors and receives nothing, so its round is "send nothing":
+// its direction bytes become kDirNone and nothing else changes.
+// Q: quiet-wave marks allocated (a.act_cur != null); the small graphs run without (Q = false).
+template <int LM, bool Q>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WAVES))) void k_ps_pull(RoundArgs a) {
-    if (gate(a, a.r)) return;
+    const unsigned long long prev = gate_count(a, a.r);  // converged after round r - 1
+    if (prev >= a.target) return;
     const Geom g = a.g;
     const uint32_t r = a.r;
+    const bool mark = Q && prev >= a.act_thr;                          // F(r) marks round r + 1
+    const bool skip = Q && r >= 2u && a.total[r - 2] >= a.act_thr;  // F(r - 1) marked round r
+    const uint8_t tag = (uint8_t)a.tag_cur;  // link_tag(r)
     uint32_t newly = 0;
     uint32_t v, end, step;
     node_range(a.lo, a.hi, a.span, v, end, step);
-    for (; v < end; v += step) newly += ps_actor<LM>(a, g, r, v);
+    for (; v < end; v += step) {
+        if (skip && a.act_prev[v >> 6] != tag) {  // wave-uniform: 64 consecutive actors
+            __builtin_nontemporal_store(kDirNone, &a.dir_cur[v]);
+            continue;
+        }
+        newly += ps_actor<LM>(a, g, r, v, mark);
+    }
     block_add(newly, a.parts, r);
 }
 
@@ -1173,10 +1193,25 @@ uint32_t span_for(uint32_t n, int grid) {
     return (s + kBlock - 1) / kBlock * kBlock;
 }
 
+// Dynamic LDS per workgroup that caps the round kernel's residency (A/B knob): 24 KB allows 6
+// workgroups (= 6 waves per SIMD) per CU's 160 KB whatever the VGPR count permits.
+#ifndef GP_PS_LDS_CAP
+#define GP_PS_LDS_CAP 0
+#endif
+
 void launch_ps_pull(const RoundArgs& a, const Launch& l) {
-    if (!a.g.has_link) hipLaunchKernelGGL(k_ps_pull<0>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
-    else if (a.rmsg_prev) hipLaunchKernelGGL(k_ps_pull<2>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
-    else hipLaunchKernelGGL(k_ps_pull<1>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+    const unsigned lds = GP_PS_LDS_CAP;
+    const bool q = a.act_cur != nullptr;
+    if (!a.g.has_link) {
+        if (q) hipLaunchKernelGGL((k_ps_pull<0, true>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
+        else hipLaunchKernelGGL((k_ps_pull<0, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
+    } else if (a.rmsg_prev) {
+        hipLaunchKernelGGL((k_ps_pull<2, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
+    } else if (q) {
+        hipLaunchKernelGGL((k_ps_pull<1, true>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
+    } else {
+        hipLaunchKernelGGL((k_ps_pull<1, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
+    }
 }
 
 void launch_gs_pull(const RoundArgs& a, const Launch& l) {

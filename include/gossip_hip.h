@@ -49,6 +49,8 @@ enum gp_flags {
     GP_FLAG_ONE_DEVICE = 8,    /* num_gpus > 1: every shard on cfg->device, exchange by device
                                   copies on one stream (tests the multi-GPU engine on one GPU) */
     GP_FLAG_GROUP = 16,        /* use the multi-GPU engine (shards + RCCL) also at num_gpus = 1 */
+    GP_FLAG_QUIET_WAVES = 32,  /* push-sum, one GPU: skip quiet waves at any graph
+                                  size (default: from 2^20 actors on); a test hook, same results */
 };
 
 typedef struct gp_config {
