@@ -1,13 +1,10 @@
-# Quiet-wave skipping with its fields in a union (kernel arguments back to 344 bytes) vs HEAD
-# (lib_base): full GPU suite, CLI times incl. the launch-latency-bound small graphs.
+# Final measurements of the round on the final tree: smoke, default bench line (C3, CPU baseline)
+# + kernel trace, C4 bench line + kernel trace, C5 one-GPU line.
 set -o pipefail
-O=$GRAFT_REPO_ROOT/gpurun_out/act4; rm -rf $O; mkdir -p $O
-TEST_TIMEOUT=800 bash tools/gpu.sh tests || exit $?
-for i in 1 2 3; do
-  for v in base new; do
-    for w in "10000000 Imp3D push-sum" "100000000 Imp3D push-sum" "100000 3D push-sum" "100000 line push-sum" "1000 full gossip"; do
-      timeout -k 10 120 cop5615-gossip_protocol_amd/lib_$v/gossip $w | grep Convergence | sed "s/^/$v $w: /" >> $O/cli.txt || exit $?
-    done
-  done
-done
-sort $O/cli.txt
+timeout -k 10 180 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.txt 2>&1 || { cat gpurun_out/smoke.txt; exit 1; }
+cat gpurun_out/smoke.txt
+OUT=c3 bash tools/gpu.sh bench || exit $?
+OUT=c4 BENCH_ARGS="--workload c4 --steps 3" bash tools/gpu.sh bench || exit $?
+mkdir -p gpurun_out/c5
+timeout -k 10 400 python3 bench.py --workload c5 --steps 2 > gpurun_out/c5/bench.json 2> gpurun_out/c5/bench.err
+rc=$?; echo "c5 rc=$rc"; cat gpurun_out/c5/bench.json; exit $rc
