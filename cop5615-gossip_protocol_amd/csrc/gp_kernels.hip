@@ -159,6 +159,11 @@ constexpr uint32_t kAblate = GP_ABLATE;
 #define GP_NT16 0
 #endif
 constexpr bool kNtStore16 = GP_NT16 != 0;
+// A/B knob: a converged actor does not read its held (S,W) (1), or reads it like the others (0).
+#ifndef GP_SKIP_CONV_HELD
+#define GP_SKIP_CONV_HELD 1
+#endif
+constexpr bool kSkipConvHeld = GP_SKIP_CONV_HELD != 0;
 
 // One 16-byte non-temporal store of a message (the round's messages cannot stay in L2 until the
 // next round reads them; streaming them leaves L2 to the rows that are re-read now).
@@ -193,10 +198,7 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
     double ss = 0.0, ww = 0.0;
     uint32_t cin = 0;
     if (r) {
-#ifndef GP_SKIP_CONV_HELD
-#define GP_SKIP_CONV_HELD 1
-#endif
-        if (!GP_SKIP_CONV_HELD) held = a.msg_prev[v];
+        if (!kSkipConvHeld) held = a.msg_prev[v];
         uint8_t d[6];
 #pragma unroll
         for (uint32_t k = 0; k < 6; ++k) d[k] = load_sel(a.dir_prev, (m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
@@ -223,7 +225,7 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
         // A converged actor only relays what arrives (program.fs:125-127): its held (S,W) and so
         // its message row are not read (more than half of the C3 run's actor-rounds).  Issued
         // with the second load level, when the flags byte has long arrived.
-        if (GP_SKIP_CONV_HELD && !(f & 16u)) held = a.msg_prev[v];
+        if (kSkipConvHeld && !(f & 16u)) held = a.msg_prev[v];
         uint32_t gi = 0;
         auto add = [&](double2 mm) {
             ss += mm.x;
