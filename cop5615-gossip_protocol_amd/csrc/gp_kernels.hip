@@ -81,6 +81,25 @@ __device__ __forceinline__ unsigned long long gate_count(const RoundArgs& A, lon
 
 __device__ __forceinline__ bool gate(const RoundArgs& A, long long a) { return gate_count(A, a) >= A.target; }
 
+// The same count computed by every wave for itself (no LDS, no block barrier): on a small graph
+// the round is one dependent chain of a few loads, and the barrier gate sits at its head.  Every
+// wave reads the same final values, so all waves of a block decide alike.
+__device__ __forceinline__ unsigned long long gate_count_wave(const RoundArgs& A, long long a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    unsigned long long x = 0;
+    if (A.sharded) {
+        x = a >= 1 ? A.total[a - 1] : 0ull;
+    } else {
+        if (a >= 1) x = *part_slot(A.parts, a - 1, lane);
+        if (a >= 2 && lane == 0u) x += A.total[a - 2];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        if (blockIdx.x == 0 && threadIdx.x == 0 && a >= 1) A.total[a - 1] = x;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 64) *part_slot(A.parts, a + 2, lane) = 0u;
+    return x;
+}
+
 // program.fs:119-143 for one actor (round 0 = :110-116): absorb, test, halve, emit.
 // Returns the new message (s,w); sets conv_now when the actor converges this round.
 struct PsOut {
@@ -322,7 +341,8 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
 // Q: quiet-wave marks allocated (a.act_cur != null); the small graphs run without (Q = false).
 template <int LM, bool Q>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WAVES))) void k_ps_pull(RoundArgs a) {
-    const unsigned long long prev = gate_count(a, a.r);  // converged after round r - 1
+    // converged after round r - 1 (one GPU, small graphs: Q = false, the per-wave gate)
+    const unsigned long long prev = (Q || LM == 2) ? gate_count(a, a.r) : gate_count_wave(a, a.r);
     if (prev >= a.target) return;
     const Geom g = a.g;
     const uint32_t r = a.r;
