@@ -202,3 +202,23 @@ def test_quiet_waves_vs_oracle(n, topo, seed):
     check_same(gpu, cpu, "push-sum")
     gpu.close()
     cpu.close()
+
+
+def test_quiet_waves_default_and_reset():
+    """Above 2^20 actors quiet-wave skipping is on by default (the kernel reports itself as the
+    marking instantiation); a run to convergence, a reset and a second run both match the
+    oracle bit for bit (the marks of the first run must not leak into the second)."""
+    n = 1_200_000
+    gpu = Simulator(n, "Imp3D", "push-sum", seed=2, kernel_timing=True)
+    assert gpu.actors >= 1 << 20
+    cpu = oracle.OracleSim(n, "Imp3D", "push-sum", seed=2)
+    cs = cpu.step(1 << 20, threads=8)
+    for _ in range(2):
+        gs = gpu.step(1 << 20)
+        assert gs.converged and (gs.round, gs.completed) == (cs.round, cs.completed)
+        np.testing.assert_array_equal(gpu.read_trace(), cpu.read_trace())
+        check_same(gpu, cpu, "push-sum")
+        assert gpu.kernel_stats()["kernel"] == "k_ps_pull<1, true>"
+        gpu.reset()
+    gpu.close()
+    cpu.close()
