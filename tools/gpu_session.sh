@@ -1,4 +1,6 @@
-# New GPU test: quiet waves on by default above 2^20 actors, across a reset.
+# Final check of the round on the committed tree: GPU suite, smoke, default bench line + trace.
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "quiet" --timeout 250 --timeout-method thread > gpurun_out/quiet_tests.log 2>&1
-rc=$?; tail -3 gpurun_out/quiet_tests.log; exit $rc
+TEST_TIMEOUT=800 bash tools/gpu.sh tests || exit $?
+timeout -k 10 180 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.txt 2>&1 || { cat gpurun_out/smoke.txt; exit 1; }
+cat gpurun_out/smoke.txt
+OUT=c3 bash tools/gpu.sh bench
