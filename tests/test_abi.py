@@ -98,3 +98,12 @@ def test_library_links_rccl():
     und = subprocess.run(["nm", "-D", "--undefined-only", _abi.LIB_PATH], capture_output=True, text=True).stdout
     for sym in ("ncclCommInitAll", "ncclSend", "ncclRecv", "ncclGroupStart", "ncclGroupEnd"):
         assert sym in und, sym
+
+
+def test_flag_values_match_header():
+    """The ctypes layer's gp_flags values are the header's (GP_FLAG_*)."""
+    text = open(_abi.HEADER).read()
+    flags = {m.group(1): int(m.group(2)) for m in re.finditer(r"GP_FLAG_(\w+)\s*=\s*(\d+)", text)}
+    assert flags, "no GP_FLAG_* in the header"
+    for name, value in flags.items():
+        assert getattr(_abi, "FLAG_" + name) == value, name
