@@ -193,6 +193,28 @@ def test_random_sweep(n, topo, algo, seed, generic):
     (8000, "3D", 2), (2000, "line", 4), (3000, "2D", 6),
 ])
 def test_quiet_waves_vs_oracle(n, topo, seed):
+    _quiet_vs_oracle(n, topo, seed)
+
+
+def _quiet_sweep_cases(count=24, seed=4242):
+    """Seeded random push-sum draws for forced quiet waves, all five topologies: line and 2D up to
+    3000 nodes (their convergence time grows fastest with N), the others log-uniform to 100000."""
+    rng = np.random.default_rng(seed)
+    topos = sorted(oracle.TOPOLOGIES)
+    out = []
+    for _ in range(count):
+        topo = topos[rng.integers(len(topos))]
+        hi = 3000 if topo in ("line", "2D") else 100000
+        out.append((int(np.exp(rng.uniform(np.log(2), np.log(hi)))), topo, int(rng.integers(1, 1 << 30))))
+    return out
+
+
+@pytest.mark.parametrize("n,topo,seed", _quiet_sweep_cases())
+def test_quiet_waves_random_sweep(n, topo, seed):
+    _quiet_vs_oracle(n, topo, seed)
+
+
+def _quiet_vs_oracle(n, topo, seed):
     gpu = Simulator(n, topo, "push-sum", seed=seed, quiet_waves=True)
     cpu = oracle.OracleSim(n, topo, "push-sum", seed=seed)
     gs = gpu.step(1 << 20)
