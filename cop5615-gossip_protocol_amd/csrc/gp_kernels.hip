@@ -183,6 +183,12 @@ constexpr bool kNtStore16 = GP_NT16 != 0;
 #define GP_SKIP_CONV_HELD 1
 #endif
 constexpr bool kSkipConvHeld = GP_SKIP_CONV_HELD != 0;
+// A/B knob: the small-graph round kernel issues its first actor's level-1 loads before the gate
+// resolves (1), or after it (0).
+#ifndef GP_EARLY_LEVEL1
+#define GP_EARLY_LEVEL1 1
+#endif
+constexpr bool kEarlyLevel1 = GP_EARLY_LEVEL1 != 0;
 
 // One 16-byte non-temporal store of a message (the round's messages cannot stay in L2 until the
 // next round reads them; streaming them leaves L2 to the rows that are re-read now).
@@ -205,27 +211,49 @@ constexpr bool kSkipConvHeld = GP_SKIP_CONV_HELD != 0;
 // LM: 0 no extra links; 1 links; 2 links on a shard of several ranks: a sender outside [lo, hi)
 // is remote, and the exchange wrote its message into the receiver's slot, rmsg_prev[slot].
 
+// Level 1 of one actor's loads (own flags, the six neighbours' direction bytes, the CSR range),
+// split out so the small-graph kernel can issue them before its gate resolves.
+struct PsLevel1 {
+    uint32_t m, li, nl;
+    uint32_t f;
+    uint32_t d[6];  // one register per byte: packing them would wait for the loads
+    double2 held;
+};
+
 template <int LM>
-__device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
-                                             bool mark = false) {
-    const uint32_t m = presence(g, v);
+__device__ __forceinline__ PsLevel1 ps_level1(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v) {
+    PsLevel1 p;
+    p.m = presence(g, v);
+    p.f = a.flags[v];
+    p.held = make_double2((double)v, 1.0);
+    p.li = 0;
+    p.nl = 0;
+    if (r) {
+        if (!kSkipConvHeld) p.held = a.msg_prev[v];
+#pragma unroll
+        for (uint32_t k = 0; k < 6; ++k) p.d[k] = load_sel(a.dir_prev, (p.m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
+        if (LM) {
+            p.li = a.rev_off[v];
+            p.nl = (kAblate & 1u) ? 0u : a.rev_off[v + 1] - p.li;
+        }
+    }
+    return p;
+}
+
+template <int LM>
+__device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
+                                              const PsLevel1& p, bool mark) {
+    const uint32_t m = p.m;
     if (!m) return 0;
     const uint32_t code = (kAblate & 8u) ? kth_bit(m, v % popc(m))
                                           : kth_bit(m, scale_draw(philox_x(v, r, kStreamPush, a.seed), popc(m)));
-    uint8_t f = a.flags[v];
-    double2 held = make_double2((double)v, 1.0);
+    uint8_t f = (uint8_t)p.f;
+    double2 held = p.held;
     double ss = 0.0, ww = 0.0;
     uint32_t cin = 0;
     if (r) {
-        if (!kSkipConvHeld) held = a.msg_prev[v];
-        uint8_t d[6];
-#pragma unroll
-        for (uint32_t k = 0; k < 6; ++k) d[k] = load_sel(a.dir_prev, (m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
-        uint32_t li = 0, nl = 0;
-        if (LM) {
-            li = a.rev_off[v];
-            nl = (kAblate & 1u) ? 0u : a.rev_off[v + 1] - li;
-        }
+        const uint32_t* d = p.d;
+        const uint32_t li = p.li, nl = p.nl;
         uint32_t hits = 0;
 #pragma unroll
         for (uint32_t k = 0; k < 6; ++k) hits |= ((m & slot_bit(k)) && d[k] == slot_code(k)) ? 1u << k : 0u;
@@ -332,6 +360,12 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
     return o.conv_now ? 1u : 0u;
 }
 
+template <int LM>
+__device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
+                                             bool mark = false) {
+    return ps_finish<LM>(a, g, r, v, ps_level1<LM>(a, g, r, v), mark);
+}
+
 // Grid-stride over the XCD-aware node range (a z-march walk, each workgroup carrying a tile up
 // through the planes so the +-G^2 rows come from L2, read 10% fewer lines but ran 12-20%
 // slower: DESIGN.md §8).
@@ -341,17 +375,36 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
 // Q: quiet-wave marks allocated (a.act_cur != null); the small graphs run without (Q = false).
 template <int LM, bool Q>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WAVES))) void k_ps_pull(RoundArgs a) {
-    // converged after round r - 1 (one GPU, small graphs: Q = false, the per-wave gate)
-    const unsigned long long prev = (Q || LM == 2) ? gate_count(a, a.r) : gate_count_wave(a, a.r);
-    if (prev >= a.target) return;
     const Geom g = a.g;
     const uint32_t r = a.r;
-    const bool mark = Q && prev >= a.act_thr;                          // F(r) marks round r + 1
-    const bool skip = Q && r >= 2u && a.total[r - 2] >= a.act_thr;  // F(r - 1) marked round r
-    const uint8_t tag = (uint8_t)a.tag_cur;  // link_tag(r)
     uint32_t newly = 0;
     uint32_t v, end, step;
     node_range(a.lo, a.hi, a.span, v, end, step);
+    if constexpr (!Q && LM != 2 && kEarlyLevel1) {
+        // Small graphs (one GPU, no quiet waves): the round is one dependent chain of loads with
+        // the gate at its head, so the first actor's level-1 loads are issued ahead of the gate's
+        // and both wait together (a thread without an actor loads actor lo's and drops them).
+        PsLevel1 p = ps_level1<LM>(a, g, r, v < end ? v : a.lo);
+        const unsigned long long prev = gate_count_wave(a, a.r);
+        if (prev >= a.target) return;
+        // keep the uses of the level-1 bytes below the gate (hoisted above it, they would wait
+        // for the loads before the gate's own loads are even issued)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) asm volatile("" : "+v"(p.d[k]));
+        asm volatile("" : "+v"(p.f));
+        if (v < end) {
+            newly += ps_finish<LM>(a, g, r, v, p, false);
+            for (v += step; v < end; v += step) newly += ps_actor<LM>(a, g, r, v);
+        }
+        block_add(newly, a.parts, r);
+        return;
+    }
+    // converged after round r - 1 (one GPU, small graphs: Q = false, the per-wave gate)
+    const unsigned long long prev = (Q || LM == 2) ? gate_count(a, a.r) : gate_count_wave(a, a.r);
+    if (prev >= a.target) return;
+    const bool mark = Q && prev >= a.act_thr;                          // F(r) marks round r + 1
+    const bool skip = Q && r >= 2u && a.total[r - 2] >= a.act_thr;  // F(r - 1) marked round r
+    const uint8_t tag = (uint8_t)a.tag_cur;  // link_tag(r)
     for (; v < end; v += step) {
         if (skip && a.act_prev[v >> 6] != tag) {  // wave-uniform: 64 consecutive actors
             __builtin_nontemporal_store(kDirNone, &a.dir_cur[v]);

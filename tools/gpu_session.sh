@@ -1,12 +1,15 @@
-# A/B: grid cap (workgroups per CU) of the round kernels with the current push-sum kernel
-# (7 resident workgroups per CU): 7 (all resident), 14, 16 (default = base), 28, 64.
+#!/bin/bash
+# A/B of the small-graph round kernel's early level-1 loads (GP_EARLY_LEVEL1), after the GPU suite.
 set -o pipefail
-O=$GRAFT_REPO_ROOT/gpurun_out/cap; rm -rf $O; mkdir -p $O
-for i in 1 2 3; do
-  for v in base c7 c14 c28 c64; do
-    for w in "10000000 Imp3D push-sum" "100000000 Imp3D push-sum" "100000000 full gossip"; do
-      timeout -k 10 120 cop5615-gossip_protocol_amd/lib_$v/gossip $w | grep Convergence | sed "s/^/$v $w: /" >> $O/cli.txt || exit $?
+O=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $O
+P=$GRAFT_REPO_ROOT/cop5615-gossip_protocol_amd
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.txt 2>&1 || { tail -20 $O/gpu_tests.txt; exit 1; }
+tail -2 $O/gpu_tests.txt
+for cfg in "100000 3D push-sum" "100000 line push-sum" "100000 2D push-sum" "100000 Imp3D push-sum" "1000 Imp3D push-sum" "300000 3D push-sum" "10000000 Imp3D push-sum"; do
+  for i in 1 2 3; do
+    for v in base early; do
+      t=$(timeout -k 10 120 $P/lib_$v/gossip $cfg | grep "Convergence Time") || exit 1
+      echo "$v $cfg: $t" | tee -a $O/ab_early.txt
     done
   done
 done
-sort $O/cli.txt
