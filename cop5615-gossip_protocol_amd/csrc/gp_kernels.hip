@@ -36,12 +36,23 @@ __device__ __forceinline__ uint32_t* part_slot(uint32_t* parts, long long a, uin
     return parts + ((uint32_t)(a & (kPartRing - 1)) * kParts + j) * kPartStride;
 }
 
+// Sum of one u32 over the 64 lanes of a full wave, wave-uniform: four DPP butterflies within
+// each row of 16 lanes (xor 1, xor 2, half-row mirror, row mirror), then the four row sums read
+// as scalars.  No LDS round trips (a __shfl_xor ladder is six dependent ds_bpermute).
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, true);  // row_half_mirror
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, true);  // row_mirror
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 0) + (uint32_t)__builtin_amdgcn_readlane((int)x, 16) +
+           (uint32_t)__builtin_amdgcn_readlane((int)x, 32) + (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+}
+
 // Block-wide sum of one u32 per thread; thread 0 adds it to this block's sub-counter of
 // round `a` (64 sub-counters on separate lines: no single-address atomic contention).
 __device__ __forceinline__ void block_add(uint32_t c, uint32_t* parts, long long a) {
     __shared__ uint32_t red[kBlock / 64];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    c = wave_sum(c);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -63,10 +74,8 @@ __device__ __forceinline__ unsigned long long gate_count(const RoundArgs& A, lon
         if (A.sharded) {
             if (threadIdx.x == 0) prev_s = a >= 1 ? A.total[a - 1] : 0ull;
         } else {
-            unsigned long long x = 0;
-            if (a >= 1) x = *part_slot(A.parts, a - 1, threadIdx.x);
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+            // one round's completions fit in u32 (at most the node count)
+            unsigned long long x = wave_sum(a >= 1 ? *part_slot(A.parts, a - 1, threadIdx.x) : 0u);
             if (threadIdx.x == 0) {
                 if (a >= 2) x += A.total[a - 2];
                 prev_s = x;
@@ -90,10 +99,9 @@ __device__ __forceinline__ unsigned long long gate_count_wave(const RoundArgs& A
     if (A.sharded) {
         x = a >= 1 ? A.total[a - 1] : 0ull;
     } else {
-        if (a >= 1) x = *part_slot(A.parts, a - 1, lane);
-        if (a >= 2 && lane == 0u) x += A.total[a - 2];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        // one round's completions fit in u32 (at most the node count)
+        x = wave_sum(a >= 1 ? *part_slot(A.parts, a - 1, lane) : 0u);
+        if (a >= 2) x += A.total[a - 2];
         if (blockIdx.x == 0 && threadIdx.x == 0 && a >= 1) A.total[a - 1] = x;
     }
     if (blockIdx.x == 0 && threadIdx.x < 64) *part_slot(A.parts, a + 2, lane) = 0u;
