@@ -197,6 +197,12 @@ constexpr bool kSkipConvHeld = GP_SKIP_CONV_HELD != 0;
 #define GP_EARLY_LEVEL1 1
 #endif
 constexpr bool kEarlyLevel1 = GP_EARLY_LEVEL1 != 0;
+// A/B knob: with the early level 1, also load all six neighbours' messages and the held (S,W)
+// there (1), or only the hits' messages at level 2 (0).
+#ifndef GP_PRE_GRID
+#define GP_PRE_GRID 1
+#endif
+constexpr bool kPreGrid = GP_PRE_GRID != 0;
 
 // One 16-byte non-temporal store of a message (the round's messages cannot stay in L2 until the
 // next round reads them; streaming them leaves L2 to the rows that are re-read now).
@@ -220,15 +226,18 @@ constexpr bool kEarlyLevel1 = GP_EARLY_LEVEL1 != 0;
 // is remote, and the exchange wrote its message into the receiver's slot, rmsg_prev[slot].
 
 // Level 1 of one actor's loads (own flags, the six neighbours' direction bytes, the CSR range),
-// split out so the small-graph kernel can issue them before its gate resolves.
+// split out so the small-graph kernel can issue them before its gate resolves.  PRE (small
+// graphs, where the round is latency-bound and bytes are cheap): also the held (S,W) and all six
+// neighbours' messages, hit or not, so the grid part of the collect needs no second level.
 struct PsLevel1 {
     uint32_t m, li, nl;
     uint32_t f;
     uint32_t d[6];  // one register per byte: packing them would wait for the loads
     double2 held;
+    double2 gm6[6];  // PRE: the six neighbours' messages (slot order)
 };
 
-template <int LM>
+template <int LM, bool PRE = false>
 __device__ __forceinline__ PsLevel1 ps_level1(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v) {
     PsLevel1 p;
     p.m = presence(g, v);
@@ -236,10 +245,16 @@ __device__ __forceinline__ PsLevel1 ps_level1(const RoundArgs& a, const Geom& g,
     p.held = make_double2((double)v, 1.0);
     p.li = 0;
     p.nl = 0;
-    if (r) {
-        if (!kSkipConvHeld) p.held = a.msg_prev[v];
+    if (PRE || r) {  // PRE: unconditional (no join for the loaded registers; ps_finish ignores
+                     // them in round 0, when the buffers hold no messages yet)
+        if (PRE || !kSkipConvHeld) p.held = a.msg_prev[v];
 #pragma unroll
         for (uint32_t k = 0; k < 6; ++k) p.d[k] = load_sel(a.dir_prev, (p.m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
+        if constexpr (PRE) {
+#pragma unroll
+            for (uint32_t k = 0; k < 6; ++k)
+                p.gm6[k] = load_sel(a.msg_prev, (p.m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
+        }
         if (LM) {
             p.li = a.rev_off[v];
             p.nl = (kAblate & 1u) ? 0u : a.rev_off[v + 1] - p.li;
@@ -248,7 +263,7 @@ __device__ __forceinline__ PsLevel1 ps_level1(const RoundArgs& a, const Geom& g,
     return p;
 }
 
-template <int LM>
+template <int LM, bool PRE = false>
 __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
                                               const PsLevel1& p, bool mark) {
     const uint32_t m = p.m;
@@ -256,7 +271,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
     const uint32_t code = (kAblate & 8u) ? kth_bit(m, v % popc(m))
                                           : kth_bit(m, scale_draw(philox_x(v, r, kStreamPush, a.seed), popc(m)));
     uint8_t f = (uint8_t)p.f;
-    double2 held = p.held;
+    double2 held = (PRE && !r) ? make_double2((double)v, 1.0) : p.held;
     double ss = 0.0, ww = 0.0;
     uint32_t cin = 0;
     if (r) {
@@ -276,11 +291,13 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
         }
         double2 gm[3];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) gm[j] = load_sel(a.msg_prev, gs[j] != 0xFFFFFFFFu, gs[j], v);
+        for (int j = 0; j < 3; ++j)
+            gm[j] = PRE ? make_double2(0.0, 0.0) : load_sel(a.msg_prev, gs[j] != 0xFFFFFFFFu, gs[j], v);
+        uint32_t pend = hits;  // PRE: grid hits not yet added
         // A converged actor only relays what arrives (program.fs:125-127): its held (S,W) and so
         // its message row are not read (more than half of the C3 run's actor-rounds).  Issued
         // with the second load level, when the flags byte has long arrived.
-        if (kSkipConvHeld && !(f & 16u)) held = a.msg_prev[v];
+        if (!PRE && kSkipConvHeld && !(f & 16u)) held = a.msg_prev[v];
         uint32_t gi = 0;
         auto add = [&](double2 mm) {
             ss += mm.x;
@@ -290,6 +307,15 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
         // Add the pending grid hits whose source is below `bound`, in ascending order.  (A
         // branch-free form with predicated exact +0.0 adds ran 1-4% slower: more VALU work.)
         auto flush = [&](uint32_t bound) {
+            if constexpr (PRE) {  // slot order = ascending source: each test is independent
+#pragma unroll
+                for (uint32_t k = 0; k < 6; ++k)
+                    if (((pend >> k) & 1u) && slot_src(g, v, k) < bound) {
+                        add(p.gm6[k]);
+                        pend &= ~(1u << k);
+                    }
+                return;
+            }
 #pragma unroll
             for (int j = 0; j < 3; ++j)
                 if (gi == (uint32_t)j && gs[j] < bound) {
@@ -392,7 +418,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WA
         // Small graphs (one GPU, no quiet waves): the round is one dependent chain of loads with
         // the gate at its head, so the first actor's level-1 loads are issued ahead of the gate's
         // and both wait together (a thread without an actor loads actor lo's and drops them).
-        PsLevel1 p = ps_level1<LM>(a, g, r, v < end ? v : a.lo);
+        PsLevel1 p = ps_level1<LM, kPreGrid>(a, g, r, v < end ? v : a.lo);
         const unsigned long long prev = gate_count_wave(a, a.r);
         if (prev >= a.target) return;
         // keep the uses of the level-1 bytes below the gate (hoisted above it, they would wait
@@ -400,8 +426,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WA
 #pragma unroll
         for (int k = 0; k < 6; ++k) asm volatile("" : "+v"(p.d[k]));
         asm volatile("" : "+v"(p.f));
+        if constexpr (kPreGrid) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) asm volatile("" : "+v"(p.gm6[k].x), "+v"(p.gm6[k].y));
+            asm volatile("" : "+v"(p.held.x), "+v"(p.held.y));
+        }
         if (v < end) {
-            newly += ps_finish<LM>(a, g, r, v, p, false);
+            newly += ps_finish<LM, kPreGrid>(a, g, r, v, p, false);
             for (v += step; v < end; v += step) newly += ps_actor<LM>(a, g, r, v);
         }
         block_add(newly, a.parts, r);
