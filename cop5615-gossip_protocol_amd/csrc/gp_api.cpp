@@ -460,7 +460,12 @@ bool fused_marks(const Handle* h) { return kFuseLinkMarks && !h->gossip && !h->g
 
 const char* round_kernel_name(const Handle* h) {
     if (full_quad(h)) return "k_gs_full4";
-    if (h->gossip) return h->generic ? "k_gs_push" : (h->g.has_link ? "k_gs_pull<true>" : "k_gs_pull<false>");
+    if (h->gossip && !h->generic) {
+        const bool e = gs_pull_early(h->args(0));
+        return h->g.has_link ? (e ? "k_gs_pull<true, true>" : "k_gs_pull<true, false>")
+                             : (e ? "k_gs_pull<false, true>" : "k_gs_pull<false, false>");
+    }
+    if (h->gossip) return "k_gs_push";
     if (h->generic) return "k_ps_push_emit";
     if (h->g.has_link) return h->rmsg[0] ? "k_ps_pull<2, false>" : h->act[0] ? "k_ps_pull<1, true>" : "k_ps_pull<1, false>";
     return h->act[0] ? "k_ps_pull<0, true>" : "k_ps_pull<0, false>";

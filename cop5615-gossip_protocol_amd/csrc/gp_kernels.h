@@ -181,6 +181,10 @@ uint32_t span_for(uint32_t n, int grid);
 // round kernels
 void launch_ps_pull(const RoundArgs& a, const Launch& l);
 void launch_gs_pull(const RoundArgs& a, const Launch& l);
+// Gossip grid rounds on graphs below 2^18 actors (one GPU) issue their level-1 loads ahead of
+// the gate: k_gs_pull<LINK, true>.  (At 1M actors the unconditional loads cost more than the
+// latency they hide: profiles/round2/ab_round_kernel.md.)
+inline bool gs_pull_early(const RoundArgs& a) { return !a.sharded && a.hi - a.lo < (1u << 18); }
 void launch_link_count(const RoundArgs& a, const Launch& l);
 void launch_ps_push_emit(const RoundArgs& a, const Launch& l);
 void launch_ps_push_fill(const RoundArgs& a, uint32_t* slot_cur, const uint32_t* boff_cur, const Launch& l);

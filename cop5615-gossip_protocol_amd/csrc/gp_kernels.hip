@@ -460,64 +460,114 @@ __device__ __forceinline__ uint32_t nib_match(uint8_t b, uint32_t code) {
     return (uint32_t)((b & 15u) == code) + (uint32_t)((b >> 4) == code);
 }
 
+// One actor's loads that do not depend on other loads (state byte, receipt counter, the six
+// neighbours' direction bytes, the CSR range).  PRE (small graphs): issued together, before the
+// gate resolves, for every actor; otherwise gs_actor loads them lazily (a done actor reads no
+// direction bytes; the counter only when something arrived).
+struct GsLevel1 {
+    uint32_t m, st, c0, li, nl;
+    uint32_t d[6];  // one register per byte: packing them would wait for the loads
+};
+
 template <bool LINK>
+__device__ __forceinline__ GsLevel1 gs_level1(const RoundArgs& a, const Geom& g, uint32_t v) {
+    GsLevel1 p;
+    p.m = presence(g, v);
+    p.st = a.gstate[v];
+    p.c0 = a.cnt[v];
+#pragma unroll
+    for (uint32_t k = 0; k < 6; ++k) p.d[k] = load_sel(a.dir_prev, (p.m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
+    p.li = 0;
+    p.nl = 0;
+    if (LINK) {
+        p.li = a.rev_off[v];
+        p.nl = a.rev_off[v + 1] - p.li;
+    }
+    return p;
+}
+
+// F(r) for one actor: apply round r-1's receipts (program.fs:92-105), emit round r (:89-95).
+template <bool LINK, bool PRE>
+__device__ __forceinline__ uint32_t gs_actor(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
+                                             const GsLevel1& p) {
+    const uint32_t m = PRE ? p.m : presence(g, v);
+    if (!m) return 0;
+    const uint8_t st = PRE ? (uint8_t)p.st : a.gstate[v];
+    uint32_t tok = st & 3u;
+    uint32_t done = (st >> 2) & 1u;
+    uint32_t newly = 0;
+    if (r && !done) {  // apply round r-1: receipts while not done at round start (program.fs:92)
+        uint32_t d[6];
+#pragma unroll
+        for (uint32_t k = 0; k < 6; ++k)
+            d[k] = PRE ? p.d[k] : load_sel(a.dir_prev, (m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
+        uint32_t inc = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 6; ++k) inc += (m & slot_bit(k)) ? nib_match((uint8_t)d[k], slot_code(k)) : 0u;
+        if (LINK) {
+            const uint32_t li = PRE ? p.li : a.rev_off[v], nl = PRE ? p.nl : a.rev_off[v + 1] - li;
+            uint8_t lc[kLinkUnroll];
+#pragma unroll
+            for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, a.slot_lo);
+#pragma unroll
+            for (uint32_t k = 0; k < kLinkUnroll; ++k)
+                if (k < nl && lc[k]) {
+                    inc += lc[k];
+                    a.lcnt_prev[li + k] = 0;
+                }
+            for (uint32_t k = kLinkUnroll; k < nl; ++k) {
+                const uint8_t c = a.lcnt_prev[li + k];
+                if (c) {
+                    inc += c;
+                    a.lcnt_prev[li + k] = 0;
+                }
+            }
+        }
+        if (inc) {
+            const uint32_t c0 = PRE ? p.c0 : a.cnt[v], c1 = c0 + inc;
+            a.cnt[v] = c1;
+            if (c0 == 0) ++tok;                                  // program.fs:99-100
+            if (c0 <= a.threshold && c1 > a.threshold) {         // program.fs:102-104
+                done = 1;
+                newly = 1;
+            }
+            a.gstate[v] = (uint8_t)(tok | (done << 2));
+        }
+    }
+    if (tok) {  // emit round r: one draw per activation chain (program.fs:89-95)
+        const uint4 x = philox(v, r, kStreamGossip, a.seed);
+        const uint32_t n = popc(m);
+        const uint32_t c0 = kth_bit(m, scale_draw(x.x, n));
+        const uint32_t c1 = tok > 1 ? kth_bit(m, scale_draw(x.y, n)) : 15u;
+        a.dir_cur[v] = (uint8_t)(c0 | (c1 << 4));
+    }
+    return newly;
+}
+
+// EARLY (graphs below 2^18 actors, one GPU): the round is one dependent chain with the gate at
+// its head, so the first actor's level-1 loads go out ahead of the gate's (as k_ps_pull does).
+template <bool LINK, bool EARLY>
 __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
-    if (a.r && gate(a, (long long)a.r - 1)) return;
     const Geom g = a.g;
     const uint32_t r = a.r;
     uint32_t v, end, step;
     node_range(a.lo, a.hi, a.span, v, end, step);
     uint32_t newly = 0;
-    for (; v < end; v += step) {
-        const uint32_t m = presence(g, v);
-        if (!m) continue;
-        const uint8_t st = a.gstate[v];
-        uint32_t tok = st & 3u;
-        uint32_t done = (st >> 2) & 1u;
-        if (r && !done) {  // apply round r-1: receipts while not done at round start (program.fs:92)
-            uint8_t d[6];
+    if constexpr (EARLY) {
+        GsLevel1 p = gs_level1<LINK>(a, g, v < end ? v : a.lo);
+        if (r && gate_count_wave(a, (long long)r - 1) >= a.target) return;
+        // keep the uses of the loaded bytes below the gate (see k_ps_pull)
+        asm volatile("" : "+v"(p.st), "+v"(p.c0));
 #pragma unroll
-            for (uint32_t k = 0; k < 6; ++k) d[k] = load_sel(a.dir_prev, (m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
-            uint32_t inc = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 6; ++k) inc += (m & slot_bit(k)) ? nib_match(d[k], slot_code(k)) : 0u;
-            if (LINK) {
-                const uint32_t li = a.rev_off[v], nl = a.rev_off[v + 1] - li;
-                uint8_t lc[kLinkUnroll];
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, a.slot_lo);
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k)
-                    if (k < nl && lc[k]) {
-                        inc += lc[k];
-                        a.lcnt_prev[li + k] = 0;
-                    }
-                for (uint32_t k = kLinkUnroll; k < nl; ++k) {
-                    const uint8_t c = a.lcnt_prev[li + k];
-                    if (c) {
-                        inc += c;
-                        a.lcnt_prev[li + k] = 0;
-                    }
-                }
-            }
-            if (inc) {
-                const uint32_t c0 = a.cnt[v], c1 = c0 + inc;
-                a.cnt[v] = c1;
-                if (c0 == 0) ++tok;                                  // program.fs:99-100
-                if (c0 <= a.threshold && c1 > a.threshold) {         // program.fs:102-104
-                    done = 1;
-                    ++newly;
-                }
-                a.gstate[v] = (uint8_t)(tok | (done << 2));
-            }
+        for (int k = 0; k < 6; ++k) asm volatile("" : "+v"(p.d[k]));
+        if (v < end) {
+            newly += gs_actor<LINK, true>(a, g, r, v, p);
+            for (v += step; v < end; v += step) newly += gs_actor<LINK, true>(a, g, r, v, gs_level1<LINK>(a, g, v));
         }
-        if (tok) {  // emit round r: one draw per activation chain (program.fs:89-95)
-            const uint4 x = philox(v, r, kStreamGossip, a.seed);
-            const uint32_t d = popc(m);
-            const uint32_t c0 = kth_bit(m, scale_draw(x.x, d));
-            const uint32_t c1 = tok > 1 ? kth_bit(m, scale_draw(x.y, d)) : 15u;
-            a.dir_cur[v] = (uint8_t)(c0 | (c1 << 4));
-        }
+    } else {
+        if (r && gate(a, (long long)r - 1)) return;
+        const GsLevel1 none{};
+        for (; v < end; v += step) newly += gs_actor<LINK, false>(a, g, r, v, none);
     }
     if (r) block_add(newly, a.parts, (long long)r - 1);
 }
@@ -1329,8 +1379,11 @@ void launch_ps_pull(const RoundArgs& a, const Launch& l) {
 }
 
 void launch_gs_pull(const RoundArgs& a, const Launch& l) {
-    if (a.g.has_link) hipLaunchKernelGGL(k_gs_pull<true>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
-    else hipLaunchKernelGGL(k_gs_pull<false>, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+    const bool e = gs_pull_early(a);
+    if (a.g.has_link && e) hipLaunchKernelGGL((k_gs_pull<true, true>), dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+    else if (a.g.has_link) hipLaunchKernelGGL((k_gs_pull<true, false>), dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+    else if (e) hipLaunchKernelGGL((k_gs_pull<false, true>), dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+    else hipLaunchKernelGGL((k_gs_pull<false, false>), dim3(l.grid), dim3(kBlock), 0, l.stream, a);
 }
 
 // Flat grids (one actor per thread): a grid-stride loop would make each iteration's load wait

@@ -48,6 +48,10 @@ def _pair(n, topo, algo, seed, **kw):
     (3000, "line", "gossip", None),
     (100000, "full", "gossip", None),
     (5000, "2D", "gossip", None),
+    # above 2^18 actors: the gossip grid kernel's lazy-load instantiation
+    (400000, "3D", "gossip", None),
+    (300000, "Imp3D", "gossip", None),
+    (300000, "2D", "gossip", 300),
 ])
 def test_vs_oracle_100k(n, topo, algo, rounds):
     gpu, cpu = _pair(n, topo, algo, seed=11)
