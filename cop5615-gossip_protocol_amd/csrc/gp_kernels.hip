@@ -63,6 +63,14 @@ __device__ __forceinline__ void block_add(uint32_t c, uint32_t* parts, long long
     }
 }
 
+// The same count added per wave (small graphs: no LDS round trip and no block barrier at the end
+// of the round; most waves have nothing to add).
+__device__ __forceinline__ void wave_add(uint32_t c, uint32_t* parts, long long a) {
+    c = wave_sum(c);
+    if ((threadIdx.x & 63u) == 0u && c)
+        atomicAdd(part_slot(parts, a, (blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kParts - 1)), c);
+}
+
 // Skip gate of a kernel that applies round `a`: the completion count after round a-1 is
 // total[a-2] + the round a-1 sub-counters, all final (earlier launches).  Every block computes
 // it (one wave, 64 loads), so every block takes the same branch; block 0 publishes total[a-1]
@@ -203,6 +211,11 @@ constexpr bool kEarlyLevel1 = GP_EARLY_LEVEL1 != 0;
 #define GP_PRE_GRID 1
 #endif
 constexpr bool kPreGrid = GP_PRE_GRID != 0;
+// A/B knob: the small-graph round kernels add their completion counts per wave (1) or per block (0).
+#ifndef GP_WAVE_ADD
+#define GP_WAVE_ADD 1
+#endif
+constexpr bool kWaveAdd = GP_WAVE_ADD != 0;
 
 // One 16-byte non-temporal store of a message (the round's messages cannot stay in L2 until the
 // next round reads them; streaming them leaves L2 to the rows that are re-read now).
@@ -435,7 +448,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WA
             newly += ps_finish<LM, kPreGrid>(a, g, r, v, p, false);
             for (v += step; v < end; v += step) newly += ps_actor<LM>(a, g, r, v);
         }
-        block_add(newly, a.parts, r);
+        if constexpr (kWaveAdd) wave_add(newly, a.parts, r);
+        else block_add(newly, a.parts, r);
         return;
     }
     // converged after round r - 1 (one GPU, small graphs: Q = false, the per-wave gate)
@@ -564,12 +578,16 @@ __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
             newly += gs_actor<LINK, true>(a, g, r, v, p);
             for (v += step; v < end; v += step) newly += gs_actor<LINK, true>(a, g, r, v, gs_level1<LINK>(a, g, v));
         }
+        if (r) {
+            if constexpr (kWaveAdd) wave_add(newly, a.parts, (long long)r - 1);
+            else block_add(newly, a.parts, (long long)r - 1);
+        }
     } else {
         if (r && gate(a, (long long)r - 1)) return;
         const GsLevel1 none{};
         for (; v < end; v += step) newly += gs_actor<LINK, false>(a, g, r, v, none);
+        if (r) block_add(newly, a.parts, (long long)r - 1);
     }
-    if (r) block_add(newly, a.parts, (long long)r - 1);
 }
 
 // ------------------------------------------------------------------ link count pass
