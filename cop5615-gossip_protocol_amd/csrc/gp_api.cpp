@@ -555,6 +555,10 @@ int launch_aux(Handle* h, int64_t k, const Xchg* x) {
 }
 
 constexpr int64_t kTimeEvery = 8;  // kernel timing: one round in 8
+#ifndef GP_TAIL_BATCH
+#define GP_TAIL_BATCH 32
+#endif
+constexpr int64_t kTailBatch = GP_TAIL_BATCH;  // rounds per batch in a run's tail (0: no tail rule)
 
 int ensure_events(Handle* h, int64_t rounds) {
     const size_t need = (size_t)(3 * rounds);
@@ -681,7 +685,11 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         } else if (timing && (rc = accumulate_timing(h, (real + kTimeEvery - 1) / kTimeEvery))) {
             return rc;
         }
-        h->batch = std::min<int64_t>(h->batch * 2, 256);
+        // Batches double up to 256 rounds; once 31/32 of the nodes have reported, the run is in
+        // its tail and the batch shrinks to GP_TAIL_BATCH, so fewer rounds are launched past
+        // convergence (each exits at its gate, but still costs a launch).
+        const bool tail = kTailBatch > 0 && h->completed * 32 >= h->lay.nodes * 31;
+        h->batch = tail ? kTailBatch : std::min<int64_t>(h->batch * 2, 256);
     }
     HIP_TRY(hipEventRecord(h->ev_b, h->stream));
     HIP_TRY(hipEventSynchronize(h->ev_b));
