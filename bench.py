@@ -16,11 +16,20 @@ Workloads:
   c4    `100000000 full gossip` to convergence (19 B per node-update roofline, int atomics).
   custom  --n / --topology / --algorithm [/ --window].
 
-N = 1: the single-GPU engine (gp_step).  N > 1 (launched by torch.distributed.run, one rank per
-GPU): node-range shards (whole z-planes), one fixed-size RCCL all-to-all per round (DESIGN.md
-§6); value = global actors x rounds / max-over-ranks wall time, and `per_rank` reports rank 0's
-round time split into round kernels / all-to-all / unpack plus the bytes it exchanges per round.
-Rank 0 prints ONE JSON line.
+N = 1: the single-GPU engine (gp_step).  N > 1, two launch forms, both split ONE graph (c5 by
+default: strong scaling) into node-range shards (whole z-planes) with one fixed-size exchange per
+round:
+  * `torch.distributed.run ... bench.py --gpus N` (the driver's form): one process per GPU, the
+    exchange is torch's all_to_all_single over RCCL;
+  * `python bench.py --gpus N` (no WORLD_SIZE): ONE process drives N GPUs through the library's
+    own multi-GPU engine (gp_config.num_gpus = N: ncclCommInitAll + grouped ncclSend/ncclRecv,
+    SURVEY.md §8b).  --one-device puts the N shards on device 0 with device copies in place of
+    RCCL (the same code path on a one-GPU box).  Fewer than N devices is an error, never a silent
+    one-GPU run.
+Either way the job first times the same window on device 0 alone with the single-GPU engine
+(`strong_scaling_base`, same job, before any shard exists), value = global actors x rounds /
+max-over-ranks wall time, and `per_rank` reports rank 0's round time.  Rank 0 prints ONE JSON
+line.
 """
 from __future__ import annotations
 
@@ -51,9 +60,15 @@ def survey_bytes_per_update(topology, algorithm):
     return 112.0 if topology == "Imp3D" else 108.0
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node: torch.distributed.run ranks, or (no WORLD_SIZE) one process "
+                         "driving N devices through the library's multi-GPU engine")
+    ap.add_argument("--one-device", action="store_true",
+                    help="--gpus N without torch.distributed: the N shards on device 0, exchange by "
+                         "device copies (tests the multi-GPU engine on a one-GPU box)")
+    ap.add_argument("--no-base", action="store_true", help="N > 1: skip the same-job one-GPU base")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=["auto", "c3", "c4", "c5", "custom"], default="auto",
@@ -68,7 +83,7 @@ def parse():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--engine", choices=["auto", "shard"], default="auto",
                     help="auto: single-GPU engine at N=1, shards at N>1; shard: shards also at N=1")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def workload(args, world):
@@ -127,9 +142,29 @@ def cpu_baseline(n, topology, algorithm, seed, budget_s, window):
     el = time.perf_counter() - t0
     value = sim.actors * rounds / el
     sim.close()
-    return {"value": value, "unit": "node-updates/s", "cores": threads, "kind": "port",
+    return {"value": value, "unit": "node-updates/s", "cores": threads, "kind": "port", "rounds": rounds,
             "sample": f"rounds 1..{rounds} of `{n} {topology} {algorithm}` seed {seed} "
                       f"({sim.actors} actors), oracle/gp_oracle.c OpenMP pull mode, {el:.1f} s"}
+
+
+def gpu_same_window(eng, rounds, reps=3):
+    """The GPU engine over the CPU sample's window (rounds 1..R of the same run, R from
+    cpu_baseline): the same-span rate a GPU/CPU ratio should use (the whole-run `value` includes
+    the cheap converged tail, which the CPU sample never reaches)."""
+    import torch
+
+    best = None
+    for _ in range(reps):
+        eng.reset()
+        eng.step(1)  # round 0, untimed as on the CPU side
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = eng.step(rounds)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        assert int(st.round) - 1 == rounds, (st.round, rounds)
+        best = el if best is None else min(best, el)
+    return eng.actors * rounds / best
 
 
 def roofline(ks, bytes_per_update, actors, wl):
@@ -152,18 +187,38 @@ def roofline(ks, bytes_per_update, actors, wl):
             "layout_frac": round(ks["bytes_per_launch"] / (ks["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
-def strong_scaling_base(name):
-    """The one-GPU point of the strong-scaling curve of workload `name` (N > 1 runs split one
-    graph): the committed N = 1 bench line of the same workload, so a reader can form the
-    efficiency against the same graph (the driver's N = 1 run is the c3 headline)."""
-    path = os.path.join(ROOT, "profiles", "round2", name, "bench_line_n1.json")
+def single_gpu_window(n_arg, topology, algorithm, seed, window, steps, warmup, device=0):
+    """The one-GPU point of a strong-scaling curve, measured in the same job before any shard
+    exists: the single-GPU engine (gp_step) on `device` over the same graph and window, then
+    freed.  Returns value (node-updates/s), ms per step and rounds per step."""
+    import torch
+
+    from gossip_amd import Simulator
+
+    cap = window if window else 1 << 40
+    stream = torch.cuda.Stream(device)
+    eng = Simulator(n_arg, topology, algorithm, seed=seed, device=device, stream=stream.cuda_stream)
     try:
-        with open(path) as f:
-            d = json.load(f)
-        return {"value": d["value"], "unit": d["unit"], "workload": d["config"]["workload"],
-                "source": os.path.relpath(path, ROOT)}
-    except (OSError, ValueError, KeyError):
-        return None
+        for _ in range(warmup):
+            eng.reset()
+            eng.step(cap)
+        rounds = 0
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.reset()
+            rounds += int(eng.step(cap).round)
+        torch.cuda.synchronize(device)
+        el = time.perf_counter() - t0
+        return {"value": eng.actors * rounds / el, "unit": "node-updates/s", "ms_per_step": el * 1e3 / steps,
+                "rounds_per_step": rounds / steps, "steps": steps,
+                "workload": f"{n_arg} {topology} {algorithm}" + (f", {window}-round window" if window else ""),
+                "engine": f"single-GPU gp_step on device {device}, same job, before the shards were built"}
+    finally:
+        eng.close()
+        del eng
+        torch.cuda.synchronize(device)
+        torch.cuda.empty_cache()
 
 
 def progress(rank, msg, t0=time.perf_counter()):
@@ -172,14 +227,139 @@ def progress(rank, msg, t0=time.perf_counter()):
         print(f"[bench {time.perf_counter() - t0:7.1f} s] {msg}", file=sys.stderr, flush=True)
 
 
-def main():
-    args = parse()
+def fail(msg):
+    print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+    raise SystemExit(2)
+
+
+def roofline_for(ks, topology, algorithm, actors, wl):
+    return roofline(ks, survey_bytes_per_update(topology, algorithm), actors, wl)
+
+
+def base_line(args, rank, n_arg, topology, algorithm, window, devices):
+    """The same-job one-GPU point (rank 0 / device 0), or None (skipped, or more nodes than one
+    GPU's 288 GB hold)."""
+    if args.no_base or rank != 0:
+        return None
+    progress(rank, "one-GPU base: the same window on device 0 alone")
+    b = single_gpu_window(n_arg, topology, algorithm, args.seed, window, args.steps, args.warmup, device=0)
+    progress(rank, f"one-GPU base: {b['value']:.3e} node-updates/s, {b['ms_per_step']:.1f} ms per step")
+    return b
+
+
+def attach_base(out, base, value, n):
+    if base:
+        base = dict(base)
+        base["t1_over_n_tn"] = value / (n * base["value"])  # = T1 / (N * TN): same rounds, same graph
+        out["strong_scaling_base"] = base
+
+
+def emit_line(args, *, name, n_arg, topology, algorithm, window, eng_actors, eng_nodes, grid, own, n_gpus, updates,
+              elapsed, rounds_total, converged, parallelism, ks, cpu=None, extra=None):
+    wl = f"{n_arg} {topology} {algorithm}"
+    out = {
+        "metric": METRIC,
+        "value": updates / elapsed,
+        "unit": "node-updates/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak" if n_gpus == 1 else "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (reference initial state S_i=i, W_i=1; Philox seed %d)" % args.seed,
+        "config": {"workload": wl + (f", {window}-round window" if window else ", to convergence"),
+                   "name": name, "actors": eng_actors, "nodes": eng_nodes,
+                   "actors_per_gpu": own, "grid": grid,
+                   "rounds_per_step": rounds_total / max(1, args.steps), "converged": converged,
+                   "parallelism": parallelism},
+        "wall_time_to_convergence_ms": elapsed * 1e3 / args.steps if not window else None,
+        "roofline": roofline_for(ks, topology, algorithm, own, wl),
+        "cpu_baseline": cpu,
+    }
+    if extra:
+        out.update(extra)
+    return out
+
+
+def main_group(args):
+    """--gpus N in ONE process: the library's multi-GPU engine (gp_config.num_gpus = N)."""
+    import torch
+
+    from gossip_amd import Simulator, sharded
+
+    N = args.gpus
+    ndev = torch.cuda.device_count()
+    if args.one_device:
+        if ndev < 1:
+            fail(f"--gpus {N} --one-device needs one GPU; {ndev} visible")
+    elif ndev < N:
+        fail(f"--gpus {N} needs {N} GPUs in this process; {ndev} visible "
+             f"(use --one-device to run the {N} shards on one GPU)")
+    name, n_arg, topology, algorithm, window = workload(args, N)
+    progress(0, f"{name}: {n_arg} {topology} {algorithm} over {N} shards "
+                f"({'one device' if args.one_device else f'{N} devices'}, library multi-GPU engine)")
+    base = base_line(args, 0, n_arg, topology, algorithm, window, ndev)
+    cap = window if window else 1 << 40
+    eng = Simulator(n_arg, topology, algorithm, seed=args.seed, device=0, num_gpus=N,
+                    one_device=args.one_device, kernel_timing=not args.no_kernel_timing)
+    bounds = sharded.partition(n_arg, topology, N)
+    own = bounds[1] - bounds[0]
+    progress(0, f"group ready ({eng.actors} actors, {own} on rank 0, {eng.layout.device_bytes / 2**30:.1f} GiB)")
+
+    def sync_all():
+        for d in range(1 if args.one_device else N):
+            torch.cuda.synchronize(d)
+
+    for _ in range(args.warmup):
+        eng.reset()
+        eng.step(cap)
+    eng.kernel_stats(reset=True)
+    rounds_total, converged = 0, True
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.reset()
+        st = eng.step(cap)
+        rounds_total += int(st.round)
+        converged &= bool(st.converged)
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    progress(0, f"{args.steps} timed step(s): {elapsed * 1e3:.1f} ms")
+    ks = eng.kernel_stats()
+    per_rank = {"actors": own, "world": N, "round_kernel_ms": ks["avg_ms"], "aux_kernel_ms": ks["aux_avg_ms"],
+                "kernel": ks["kernel"], "aux_kernel": ks["aux_kernel"], "sampled_rounds": ks["launches"]}
+    transport = ("device copies on one GPU (GP_FLAG_ONE_DEVICE: the multi-GPU code path, no RCCL)"
+                 if args.one_device else "RCCL ncclCommInitAll + grouped ncclSend/ncclRecv")
+    out = emit_line(args, name=name, n_arg=n_arg, topology=topology, algorithm=algorithm, window=window,
+                    eng_actors=eng.actors, eng_nodes=eng.nodes, grid=int(eng.layout.grid), own=own, n_gpus=N,
+                    updates=float(eng.actors) * rounds_total, elapsed=elapsed, rounds_total=rounds_total,
+                    converged=converged,
+                    parallelism=f"node-range shards x{N}, one process, library multi-GPU engine; exchange: {transport}",
+                    ks=ks, extra={"per_rank": per_rank, "devices": 1 if args.one_device else N,
+                                  "launch": "one process (gp_config.num_gpus)"})
+    attach_base(out, base, out["value"], N)
+    print(json.dumps(out), flush=True)
+    eng.close()
+    return out
+
+
+def main(argv=None):
+    args = parse(argv)
     import torch
     import torch.distributed as dist
 
+    if args.gpus < 1:
+        fail("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return main_group(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and args.gpus != 1:
+        fail(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     use_shards = world > 1 or args.engine == "shard"
     if use_shards:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -192,9 +372,12 @@ def main():
 
     name, n_arg, topology, algorithm, window = workload(args, world)
     progress(rank, f"{name}: {n_arg} {topology} {algorithm} on {world} GPU(s)")
+    base = None
+    if world > 1:  # rank 0 times the window on its GPU alone while the other ranks wait
+        base = base_line(args, rank, n_arg, topology, algorithm, window, torch.cuda.device_count())
+        dist.barrier()
     cap = window if window else 1 << 40
     timing = not args.no_kernel_timing
-    timer = None
     if use_shards:
         eng = sharded.HipShard(n_arg, topology, algorithm, rank=rank, world=world, seed=args.seed,
                                device=local, kernel_timing=timing)
@@ -250,44 +433,26 @@ def main():
         one_step(timer)
         per_rank = dict(timer.means(), actors=own, bytes_sent_per_round=sum(eng.send_splits),
                         bytes_received_per_round=sum(eng.recv_splits), world=world)
-    wl = f"{n_arg} {topology} {algorithm}"
     out = None
     if rank == 0:
-        roof = roofline(ks, survey_bytes_per_update(topology, algorithm), own, wl)
         cpu = None
         # the oracle holds the whole graph in host memory and builds it serially: beyond ~2e8
         # nodes its setup alone outlasts a bounded sample, so C5 (1e9) reports none
         if world == 1 and not args.no_cpu_baseline and n_arg <= CPU_BASELINE_MAX_N:
             progress(rank, "CPU baseline sample")
             cpu = cpu_baseline(n_arg, topology, algorithm, args.seed, args.cpu_seconds, window)
-        rounds_per_step = rounds_total / max(1, args.steps)
-        scaling = "weak" if world == 1 else "strong"
-        out = {
-            "metric": METRIC,
-            "value": updates / elapsed,
-            "unit": "node-updates/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed * 1e3 / args.steps,
-            "higher_is_better": True,
-            "scaling": scaling,
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (reference initial state S_i=i, W_i=1; Philox seed %d)" % args.seed,
-            "config": {"workload": wl + (f", {window}-round window" if window else ", to convergence"),
-                       "name": name, "actors": eng.actors, "nodes": eng.nodes,
-                       "actors_per_gpu": own, "grid": int(eng.layout.grid),
-                       "rounds_per_step": rounds_per_step, "converged": converged,
-                       "parallelism": f"node-range shards x{world}, RCCL all-to-all" if use_shards else "single"},
-            "wall_time_to_convergence_ms": elapsed * 1e3 / args.steps if not window else None,
-            "roofline": roof,
-            "cpu_baseline": cpu,
-        }
-        if per_rank:
-            out["per_rank"] = per_rank
+            if not use_shards:  # the GPU over the same rounds, for a same-span ratio
+                cpu["gpu_value_same_rounds"] = gpu_same_window(eng, cpu["rounds"])
+                cpu["gpu_over_cpu_same_rounds"] = cpu["gpu_value_same_rounds"] / cpu["value"]
+        par = f"node-range shards x{world}, RCCL all-to-all" if use_shards else "single"
+        out = emit_line(args, name=name, n_arg=n_arg, topology=topology, algorithm=algorithm, window=window,
+                        eng_actors=eng.actors, eng_nodes=eng.nodes, grid=int(eng.layout.grid), own=own,
+                        n_gpus=world, updates=updates, elapsed=elapsed, rounds_total=rounds_total,
+                        converged=converged, parallelism=par, ks=ks, cpu=cpu,
+                        extra={"per_rank": per_rank} if per_rank else None)
         if world > 1:
-            out["strong_scaling_base"] = strong_scaling_base(name)
+            out["launch"] = "torch.distributed.run, one process per GPU"
+            attach_base(out, base, out["value"], world)
         print(json.dumps(out), flush=True)
     eng.close()
     if use_shards:

@@ -3,8 +3,9 @@
 // Host orchestration only: sizes and geometry (program.fs:26-31, 150-313), device buffers,
 // the round loop that replaces the actor dispatch (program.fs:82-146) and the ParentActor
 // count (program.fs:44-63), and state read-back.  All per-actor work runs in gp_kernels.hip.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
+#include <rccl/rccl.h>  // types only: RCCL itself is loaded on first use (Rccl below)
 
 // Quiet-wave skipping of the push-sum round kernel (one GPU, from kQuietMinActors actors or under
 // GP_FLAG_QUIET_WAVES): the marks are kept once this percentage of the nodes has converged (0:
@@ -628,6 +629,8 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
     int rc;
     while (!h->converged && h->rounds < goal) {
         const int64_t B = std::min<int64_t>(h->batch, goal - h->rounds);
+        const int64_t before = h->completed;
+        const bool was_tail = kTailBatch > 0 && before * 32 >= h->lay.nodes * 31;
         if ((rc = ensure_trace(h, h->next_kernel + B + 4))) return rc;
         if (h->gossip && h->next_kernel == 0) {  // F(0) only emits round 0
             if ((rc = launch_round(h, 0, nullptr, false, 0))) return rc;
@@ -687,9 +690,13 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         }
         // Batches double up to 256 rounds; once 31/32 of the nodes have reported, the run is in
         // its tail and the batch shrinks to GP_TAIL_BATCH, so fewer rounds are launched past
-        // convergence (each exits at its gate, but still costs a launch).
+        // convergence (each exits at its gate, but still costs a launch).  A tail batch that
+        // completed no node doubles again (a long quiet tail, e.g. line gossip, would otherwise
+        // pay a host sync every GP_TAIL_BATCH rounds).
         const bool tail = kTailBatch > 0 && h->completed * 32 >= h->lay.nodes * 31;
-        h->batch = tail ? kTailBatch : std::min<int64_t>(h->batch * 2, 256);
+        if (!tail) h->batch = std::min<int64_t>(h->batch * 2, 256);
+        else if (!was_tail || h->completed != before) h->batch = kTailBatch;
+        else h->batch = std::min<int64_t>(h->batch * 2, 256);
     }
     HIP_TRY(hipEventRecord(h->ev_b, h->stream));
     HIP_TRY(hipEventSynchronize(h->ev_b));
@@ -1129,6 +1136,41 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
 //     sending / receiving shard's stream, so kernels and transfers stay stream-ordered;
 //   * GP_FLAG_ONE_DEVICE (tests on one GPU): every shard on cfg->device, one shared stream,
 //     the chunks moved by device copies.
+// RCCL is opened on first use (a multi-device group), not linked: the one-GPU engine and the CLI
+// load on an install without RCCL.  In a torch process dlopen by soname returns the RCCL torch
+// has already loaded, so the process keeps one copy.
+struct Rccl {
+    decltype(&ncclCommInitAll) comm_init_all = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+const Rccl* rccl() {
+    static Rccl r;
+    static bool tried = false;
+    if (!tried) {
+        tried = true;
+        void* so = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!so) so = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (so) {
+            r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(dlsym(so, "ncclCommInitAll"));
+            r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(so, "ncclCommDestroy"));
+            r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(so, "ncclGroupStart"));
+            r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(so, "ncclGroupEnd"));
+            r.send = reinterpret_cast<decltype(r.send)>(dlsym(so, "ncclSend"));
+            r.recv = reinterpret_cast<decltype(r.recv)>(dlsym(so, "ncclRecv"));
+            r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(so, "ncclGetErrorString"));
+        }
+    }
+    const bool ok = r.comm_init_all && r.comm_destroy && r.group_start && r.group_end && r.send && r.recv &&
+                    r.error_string;
+    return ok ? &r : nullptr;
+}
+
 struct Group {
     int W = 0;
     bool one_device = false;
@@ -1147,7 +1189,7 @@ struct Group {
             if (shard[p]) (void)hipStreamSynchronize(shard[p]->stream);
         }
         for (ncclComm_t c : comm)
-            if (c) (void)ncclCommDestroy(c);
+            if (c) (void)rccl()->comm_destroy(c);  // a communicator exists only if RCCL loaded
         for (size_t p = 0; p < shard.size(); ++p) {
             if (!one_device) (void)hipSetDevice(dev[p]);
             if (p < send.size() && send[p]) (void)hipFree(send[p]);
@@ -1158,11 +1200,27 @@ struct Group {
     }
 };
 
-#define RCCL_TRY(x)                                                                                \
-    do {                                                                                           \
-        ncclResult_t r_ = (x);                                                                     \
-        if (r_ != ncclSuccess) return fail(GP_ERCCL, "%s failed: %s", #x, ncclGetErrorString(r_)); \
+#define RCCL_TRY(x)                                                                                      \
+    do {                                                                                                 \
+        ncclResult_t r_ = (x);                                                                           \
+        if (r_ != ncclSuccess) return fail(GP_ERCCL, "%s failed: %s", #x, rccl()->error_string(r_));    \
     } while (0)
+
+// Send / receive pairs of every (p, q) between ncclGroupStart and ncclGroupEnd.  An error inside
+// the group still closes it (the group is left open otherwise, and the next RCCL call fails).
+int group_exchange_rccl(Group& G, const Rccl& R) {
+    const int W = G.W;
+    for (int p = 0; p < W; ++p) {
+        const Handle* s = G.shard[p];
+        for (int q = 0; q < W; ++q) {
+            if (q == p) continue;
+            const size_t ns = s->out_chunk[q].size, nr = s->in_chunk[q].size;
+            if (ns) RCCL_TRY(R.send(static_cast<char*>(G.send[p]) + s->out_off[q], ns, ncclUint8, q, G.comm[p], s->stream));
+            if (nr) RCCL_TRY(R.recv(static_cast<char*>(G.recv[p]) + s->in_off[q], nr, ncclUint8, q, G.comm[p], s->stream));
+        }
+    }
+    return GP_OK;
+}
 
 int group_exchange(Group& G) {
     const int W = G.W;
@@ -1177,17 +1235,12 @@ int group_exchange(Group& G) {
             }
         return GP_OK;
     }
-    RCCL_TRY(ncclGroupStart());
-    for (int p = 0; p < W; ++p) {
-        const Handle* s = G.shard[p];
-        for (int q = 0; q < W; ++q) {
-            if (q == p) continue;
-            const size_t ns = s->out_chunk[q].size, nr = s->in_chunk[q].size;
-            if (ns) RCCL_TRY(ncclSend(static_cast<char*>(G.send[p]) + s->out_off[q], ns, ncclUint8, q, G.comm[p], s->stream));
-            if (nr) RCCL_TRY(ncclRecv(static_cast<char*>(G.recv[p]) + s->in_off[q], nr, ncclUint8, q, G.comm[p], s->stream));
-        }
-    }
-    RCCL_TRY(ncclGroupEnd());
+    const Rccl& R = *rccl();  // loaded: the group has communicators
+    RCCL_TRY(R.group_start());
+    const int rc = group_exchange_rccl(G, R);
+    const ncclResult_t end = R.group_end();
+    if (rc) return rc;
+    if (end != ncclSuccess) return fail(GP_ERCCL, "ncclGroupEnd failed: %s", R.error_string(end));
     return GP_OK;
 }
 
@@ -1286,12 +1339,19 @@ int group_create(const gp_config* cfg, gp_layout* out, void** handle) {
                              cfg->device, d, ndev));
         G.dev.push_back(d);
     }
+    // every failure below goes through bail(): the shards, streams and buffers built so far are freed
+    auto set_dev = [&](int d) {
+        const hipError_t e = hipSetDevice(d);
+        return e == hipSuccess ? GP_OK : fail(GP_EHIP, "hipSetDevice(%d): %s", d, hipGetErrorString(e));
+    };
+    int rc;
     if (G.one_device) {
-        HIP_TRY(hipSetDevice(cfg->device));
+        if ((rc = set_dev(cfg->device))) return bail(rc);
         hipError_t e = hipStreamCreateWithFlags(&G.shared, hipStreamNonBlocking);
         if (e != hipSuccess) return bail(fail(GP_EHIP, "hipStreamCreate: %s", hipGetErrorString(e)));
+    } else if (!rccl()) {
+        return bail(fail(GP_ERCCL, "num_gpus %d needs RCCL: librccl.so.1 could not be loaded (%s)", W, dlerror()));
     }
-    int rc;
     G.shard.assign((size_t)W, nullptr);
     G.send.assign((size_t)W, nullptr);
     G.recv.assign((size_t)W, nullptr);
@@ -1311,7 +1371,7 @@ int group_create(const gp_config* cfg, gp_layout* out, void** handle) {
         if ((rc = create(&c, p, W, true, &lay, nullptr, &sh))) return bail(rc);
         Handle* s = H(sh);
         G.shard[p] = s;
-        HIP_TRY(hipSetDevice(G.dev[p]));
+        if ((rc = set_dev(G.dev[p]))) return bail(rc);
         if (s->send_total && hipMalloc(&G.send[p], (size_t)s->send_total) != hipSuccess)
             return bail(fail(GP_ENOMEM, "exchange send buffer of %lld bytes", (long long)s->send_total));
         if (s->recv_total && hipMalloc(&G.recv[p], (size_t)s->recv_total) != hipSuccess)
@@ -1321,10 +1381,10 @@ int group_create(const gp_config* cfg, gp_layout* out, void** handle) {
     }
     if (!G.one_device) {
         G.comm.assign((size_t)W, nullptr);
-        ncclResult_t r = ncclCommInitAll(G.comm.data(), W, G.dev.data());
+        ncclResult_t r = rccl()->comm_init_all(G.comm.data(), W, G.dev.data());
         if (r != ncclSuccess) {
             G.comm.clear();
-            return bail(fail(GP_ERCCL, "ncclCommInitAll(%d devices): %s", W, ncclGetErrorString(r)));
+            return bail(fail(GP_ERCCL, "ncclCommInitAll(%d devices): %s", W, rccl()->error_string(r)));
         }
     }
     h->cfg = *cfg;

@@ -185,10 +185,20 @@ constexpr uint32_t kLinkUnroll = GP_LINK_UNROLL;
 // product is built with 0, and the results of any other value are wrong by construction.
 // bit 0: no extra-link collect; bit 3: no Philox draw; bit 4: no grid-hit messages; bit 5: full
 // gossip receipts as plain random stores instead of atomics.
+// Stream attribution (push-sum round kernel): the load still issues, at an index folded into a
+// 4096-element, cache-resident prefix of its array, so the stream's HBM lines drop out while the
+// instruction mix stays: bit 6 held row, 7 the six neighbours' direction bytes, 8 flags, 9 CSR
+// offsets (li = v, nl = 1 instead), 10 CSR sources, 11 link marks, 12 lpos, 13 fired-link
+// message gathers, 14 grid-hit message gathers, 15 only the +-G^2 grid-hit gathers, 16 only the
+// +-G^2 direction bytes.
 #ifndef GP_ABLATE
 #define GP_ABLATE 0
 #endif
 constexpr uint32_t kAblate = GP_ABLATE;
+template <uint32_t BIT>
+__device__ __forceinline__ uint32_t ab(uint32_t i) {
+    return (kAblate & BIT) ? (i & 0xFFFu) : i;
+}
 // A/B knob: the message as one 16-byte non-temporal store (1) or two 8-byte ones (0).
 #ifndef GP_NT16
 #define GP_NT16 0
@@ -254,23 +264,32 @@ template <int LM, bool PRE = false>
 __device__ __forceinline__ PsLevel1 ps_level1(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v) {
     PsLevel1 p;
     p.m = presence(g, v);
-    p.f = a.flags[v];
+    p.f = a.flags[ab<256u>(v)];
     p.held = make_double2((double)v, 1.0);
     p.li = 0;
     p.nl = 0;
     if (PRE || r) {  // PRE: unconditional (no join for the loaded registers; ps_finish ignores
                      // them in round 0, when the buffers hold no messages yet)
-        if (PRE || !kSkipConvHeld) p.held = a.msg_prev[v];
+        if (PRE || !kSkipConvHeld) p.held = a.msg_prev[ab<64u>(v)];
 #pragma unroll
-        for (uint32_t k = 0; k < 6; ++k) p.d[k] = load_sel(a.dir_prev, (p.m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
+        for (uint32_t k = 0; k < 6; ++k) {
+            const uint32_t u = slot_src(g, v, k);
+            const uint32_t i = (k == 0 || k == 5) ? ab<65536u>(ab<128u>(u)) : ab<128u>(u);
+            p.d[k] = load_sel(a.dir_prev, (p.m & slot_bit(k)) != 0u, i, ab<128u>(v));
+        }
         if constexpr (PRE) {
 #pragma unroll
             for (uint32_t k = 0; k < 6; ++k)
                 p.gm6[k] = load_sel(a.msg_prev, (p.m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
         }
         if (LM) {
-            p.li = a.rev_off[v];
-            p.nl = (kAblate & 1u) ? 0u : a.rev_off[v + 1] - p.li;
+            if (kAblate & 512u) {
+                p.li = v;
+                p.nl = 1u;
+            } else {
+                p.li = a.rev_off[v];
+                p.nl = (kAblate & 1u) ? 0u : a.rev_off[v + 1] - p.li;
+            }
         }
     }
     return p;
@@ -305,12 +324,16 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
         double2 gm[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-            gm[j] = PRE ? make_double2(0.0, 0.0) : load_sel(a.msg_prev, gs[j] != 0xFFFFFFFFu, gs[j], v);
+            gm[j] = PRE ? make_double2(0.0, 0.0)
+                        : load_sel(a.msg_prev, gs[j] != 0xFFFFFFFFu,
+                                   (gs[j] == v - g.plane || gs[j] == v + g.plane) ? ab<32768u>(ab<16384u>(gs[j]))
+                                                                                : ab<16384u>(gs[j]),
+                                   v);
         uint32_t pend = hits;  // PRE: grid hits not yet added
         // A converged actor only relays what arrives (program.fs:125-127): its held (S,W) and so
         // its message row are not read (more than half of the C3 run's actor-rounds).  Issued
         // with the second load level, when the flags byte has long arrived.
-        if (!PRE && kSkipConvHeld && !(f & 16u)) held = a.msg_prev[v];
+        if (!PRE && kSkipConvHeld && !(f & 16u)) held = a.msg_prev[ab<64u>(v)];
         uint32_t gi = 0;
         auto add = [&](double2 mm) {
             ss += mm.x;
@@ -348,12 +371,12 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
         if (LM) {
             uint32_t ls[kLinkUnroll];
 #pragma unroll
-            for (uint32_t k = 0; k < kLinkUnroll; ++k) ls[k] = load_sel(a.rev_src, k < nl, li + k, a.slot_lo);
+            for (uint32_t k = 0; k < kLinkUnroll; ++k) ls[k] = load_sel(a.rev_src, k < nl, ab<1024u>(li + k), a.slot_lo);
             bool lk[kLinkUnroll];
             double2 lm[kLinkUnroll];
             uint8_t lc[kLinkUnroll];
 #pragma unroll
-            for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, li + k, a.slot_lo);
+            for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, ab<2048u>(li + k), a.slot_lo);
             // ---- level 3: the messages of the sources whose slot is marked
 #pragma unroll
             for (uint32_t k = 0; k < kLinkUnroll; ++k) {
@@ -361,7 +384,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                 if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
                     lm[k] = a.rmsg_prev[li + k];
                 } else {
-                    lm[k] = load_sel(a.msg_prev, lk[k], ls[k], v);
+                    lm[k] = load_sel(a.msg_prev, lk[k], ab<8192u>(ls[k]), v);
                 }
             }
 #pragma unroll
@@ -395,7 +418,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
     }
     __builtin_nontemporal_store(o.send ? (uint8_t)code : kDirNone, &a.dir_cur[v]);
     if constexpr (LM == 1 && kFuseLinkMarks) {  // the link pass's mark, written by the sender
-        if (o.send && code == kDirLink) a.lcnt_cur[a.lpos[v]] = (uint8_t)a.tag_cur;
+        if (o.send && code == kDirLink) a.lcnt_cur[a.lpos[ab<4096u>(v)]] = (uint8_t)a.tag_cur;
     }
     if (f != f0) a.flags[v] = f;
     if (o.conv_now) a.frozen[v] = o.msg;

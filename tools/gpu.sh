@@ -7,6 +7,7 @@
 #   pmc     FETCH_SIZE and WRITE_SIZE passes (one run each) over 60 rounds of prof_run.py
 #   loop    kernel trace of W loopback shards of one graph (tools/shard_loopback_prof.py $LOOP_ARGS)
 #   ab      kernel-trace A/B of the variant libraries named in $VARIANTS (lib_<name>/, GP_LIB)
+#   abpmc   one FETCH_SIZE pass per variant library of $VARIANTS over $ROUNDS (default 60) rounds
 # Extra prof_run.py arguments: $PROF_ARGS; rounds: $ROUNDS; bench.py arguments: $BENCH_ARGS;
 # output directory name: $OUT (default: the mode).
 set -o pipefail
@@ -48,6 +49,12 @@ case $MODE in
   ab)
     for v in ${VARIANTS}; do
       GP_LIB=lib_$v kt "kt_$v" python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-300} ${PROF_ARGS} || exit $?
+    done ;;
+  abpmc)
+    for v in ${VARIANTS}; do
+      ( cd /tmp && export TMPDIR=/tmp && GP_LIB=lib_$v timeout -s KILL 90 rocprofv3 --pmc ${PMC_COUNTERS:-FETCH_SIZE} --output-format csv -d "$O/pmc_$v" -o p -- python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-60} ${PROF_ARGS} > "$O/pmc_$v.log" 2>&1 )
+      rc=$?; echo "pmc $v rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      python3 "$R/tools/pmc_summary.py" "$O/pmc_$v" k_ps_pull | sed "s/^/$v /"
     done ;;
   *) echo "unknown mode $MODE"; exit 2 ;;
 esac
