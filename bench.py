@@ -64,7 +64,8 @@ def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
                     help="GPUs of this node: torch.distributed.run ranks, or (no WORLD_SIZE) one process "
-                         "driving N devices through the library's multi-GPU engine")
+                         "driving N devices through the library's multi-GPU engine (bit-exact with N shards "
+                         "on one GPU; an RCCL exchange between physical GPUs is untested so far)")
     ap.add_argument("--one-device", action="store_true",
                     help="--gpus N without torch.distributed: the N shards on device 0, exchange by "
                          "device copies (tests the multi-GPU engine on a one-GPU box)")
@@ -98,24 +99,26 @@ def workload(args, world):
 
 def pmc_traffic(kernels, wl: str):
     """HBM bytes per round of `kernels` (summed) from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic.json {workload: {kernel: ...}}, made by tools/make_pmc_traffic.py), or
-    None when the workload or a kernel has no entry."""
+    (profiles/pmc_traffic.json {workload: {kernel: ...}}, made by tools/pmc_run_summary.py over a
+    whole run, or tools/make_pmc_traffic.py), and the rounds that figure covers; (None, None) when
+    the workload or a kernel has no entry."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, None
     per = d.get(wl)
     if not isinstance(per, dict):
-        return None
-    total = 0.0
+        return None, None
+    total, spans = 0.0, []
     for k in kernels:
         e = per.get(k)
         if not e:
-            return None
+            return None, None
         total += e["hbm_bytes_per_launch"]
-    return total
+        spans.append(e.get("rounds", "median of the first 60 rounds"))
+    return total, "; ".join(sorted(set(spans)))
 
 
 def cpu_baseline(n, topology, algorithm, seed, budget_s, window):
@@ -177,9 +180,12 @@ def roofline(ks, bytes_per_update, actors, wl):
     algo_bytes = bytes_per_update * actors
     achieved = algo_bytes / (round_ms * 1e-3) / 1e9
     kernels = [ks["kernel"]] + ([ks["aux_kernel"]] if ks["aux_kernel"] else [])
-    traffic = pmc_traffic(kernels, wl)
+    traffic, traffic_rounds = pmc_traffic(kernels, wl)
+    # measured HBM bytes (PMC) over their rounds' mean time: the fraction of peak the kernel moves
+    measured = traffic / (round_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_rounds": traffic_rounds,
+            "hbm_measured_frac": round(measured, 4) if measured else None,
             "kernel": " + ".join(kernels), "avg_kernel_ms": round(ks["avg_ms"], 5),
             "avg_aux_ms": round(ks["aux_avg_ms"], 5), "round_ms": round(round_ms, 5),
             "bytes_per_launch": algo_bytes, "bytes_per_update": bytes_per_update, "launches": ks["launches"],

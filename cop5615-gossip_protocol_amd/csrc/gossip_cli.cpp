@@ -12,7 +12,8 @@
 // (actors, nodes, leader) after the banner.
 //
 // --gpus N runs the one graph over N GPUs of this process (gp_config.num_gpus: node-range
-// shards, RCCL exchange inside the library).  --mode round is the synchronous-round engine (the
+// shards, RCCL exchange inside the library; bit-exact with several shards on one GPU, but an
+// exchange between physical GPUs is untested so far: README.md).  --mode round is the synchronous-round engine (the
 // only mode); the reference's asynchronous actor execution is not part of the engine: its
 // statistical restatement is test infrastructure (oracle/gp_async.c), so --mode async is
 // refused.
@@ -54,7 +55,9 @@ int main(int argc, char** argv) {
     if (argc < 4) {
         std::fprintf(stderr,
                      "usage: %s numNodes topology algorithm [--seed S] [--max-rounds R] [--device D] [--gpus N] "
-                     "[--mode round] [--verbose] [--trace FILE]\n",
+                     "[--mode round] [--verbose] [--trace FILE]\n"
+                     "  --gpus N: one graph over N GPUs of this process (RCCL inside the library; an exchange\n"
+                     "            between physical GPUs has not been tested yet, see README.md)\n",
                      argv[0]);
         return 2;
     }

@@ -85,7 +85,7 @@ struct FastDiv {
     uint32_t d, m, s1, s2;
 };
 
-inline FastDiv make_fastdiv(uint32_t d) {
+__host__ __device__ inline FastDiv make_fastdiv(uint32_t d) {
     uint32_t l = 0;
     while (l < 32 && (1ull << l) < d) ++l;  // l = ceil(log2 d)
     FastDiv f;

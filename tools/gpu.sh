@@ -8,6 +8,11 @@
 #   loop    kernel trace of W loopback shards of one graph (tools/shard_loopback_prof.py $LOOP_ARGS)
 #   ab      kernel-trace A/B of the variant libraries named in $VARIANTS (lib_<name>/, GP_LIB)
 #   abpmc   one FETCH_SIZE pass per variant library of $VARIANTS over $ROUNDS (default 60) rounds
+#   cli     CLI convergence times of the variant libraries of $VARIANTS on each workload of
+#           $CLI_CASES ("N topo algo;N topo algo"), $REPS (default 3) interleaved runs
+#   loopab  `loop` for each variant library of $VARIANTS
+#   pmcrun  FETCH_SIZE and WRITE_SIZE passes over a whole run (prof_run.py, $ROUNDS default: to
+#           convergence) -> tools/pmc_run_summary.py ($PMC_WORKLOAD, $PMC_KERNEL) into $O
 # Extra prof_run.py arguments: $PROF_ARGS; rounds: $ROUNDS; bench.py arguments: $BENCH_ARGS;
 # output directory name: $OUT (default: the mode).
 set -o pipefail
@@ -55,6 +60,26 @@ case $MODE in
       ( cd /tmp && export TMPDIR=/tmp && GP_LIB=lib_$v timeout -s KILL 90 rocprofv3 --pmc ${PMC_COUNTERS:-FETCH_SIZE} --output-format csv -d "$O/pmc_$v" -o p -- python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-60} ${PROF_ARGS} > "$O/pmc_$v.log" 2>&1 )
       rc=$?; echo "pmc $v rc=$rc"; [ $rc -eq 0 ] || exit $rc
       python3 "$R/tools/pmc_summary.py" "$O/pmc_$v" k_ps_pull | sed "s/^/$v /"
+    done ;;
+  pmcrun)
+    for c in FETCH_SIZE WRITE_SIZE; do
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_$c" -o p -- python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-1000000} ${PROF_ARGS} > "$O/pmc_$c.log" 2>&1 )
+      rc=$?; echo "pmc $c rc=$rc"; tail -1 "$O/pmc_$c.log"; [ $rc -eq 0 ] || exit $rc
+    done
+    python3 "$R/tools/pmc_run_summary.py" "$O/pmc_FETCH_SIZE" "$O/pmc_WRITE_SIZE" "$O/pmc_run.json" "${PMC_WORKLOAD:-10000000 Imp3D push-sum}" "${PMC_KERNEL:-k_ps_pull<1, true>}" ;;
+  cli)
+    IFS=';' read -ra CASES <<< "${CLI_CASES:-10000000 Imp3D push-sum}"
+    for c in "${CASES[@]}"; do
+      for i in $(seq ${REPS:-3}); do
+        for v in ${VARIANTS}; do
+          out=$(timeout -k 10 120 "$R/cop5615-gossip_protocol_amd/lib_$v/gossip" $c < /dev/null) || { echo "cli $v $c failed"; exit 1; }
+          echo "$v $c: $(echo "$out" | grep -E 'Convergence Time|Rounds' | tr '\n' ' ')" | tee -a "$O/cli.txt"
+        done
+      done
+    done ;;
+  loopab)
+    for v in ${VARIANTS}; do
+      GP_LIB=lib_$v kt "kt_$v" python3 "$R/tools/shard_loopback_prof.py" ${LOOP_ARGS} || exit $?
     done ;;
   *) echo "unknown mode $MODE"; exit 2 ;;
 esac
