@@ -457,11 +457,7 @@ int reset(Handle* h) {
 // Full gossip on one GPU runs the four-actors-per-lane kernel with the done bitmap.
 bool full_quad(const Handle* h) { return h->gossip && h->full && !h->sharded && h->lo == 0; }
 
-// Push-sum link marks written by the round kernel itself (one GPU: kFuseLinkMarks; shards always:
-// k_ps_pull_x also writes the exchange entries).
-bool fused_marks(const Handle* h) {
-    return !h->gossip && !h->generic && h->g.has_link && (h->sharded || kFuseLinkMarks);
-}
+bool fused_marks(const Handle* h) { return kFuseLinkMarks && !h->gossip && !h->generic && !h->sharded && h->g.has_link; }
 
 const char* round_kernel_name(const Handle* h) {
     if (full_quad(h)) return "k_gs_full4";
@@ -472,14 +468,16 @@ const char* round_kernel_name(const Handle* h) {
     }
     if (h->gossip) return "k_gs_push";
     if (h->generic) return "k_ps_push_emit";
-    if (h->g.has_link) return h->rmsg[0] ? "k_ps_pull_x<2>" : h->act[0] ? "k_ps_pull<1, true>" : "k_ps_pull<1, false>";
-    return h->act[0] ? "k_ps_pull<0, true>" : "k_ps_pull<0, false>";
+    if (h->sharded && h->g.has_link) return h->rmsg[0] ? "k_ps_pull<2, false>" : "k_ps_pull<1, false>";
+    const bool slab = ps_slab_walk(h->args(0));
+    if (h->g.has_link) return slab ? "k_ps_slab<1>" : h->act[0] ? "k_ps_pull<1, true>" : "k_ps_pull<1, false>";
+    return slab ? "k_ps_slab<0>" : h->act[0] ? "k_ps_pull<0, true>" : "k_ps_pull<0, false>";
 }
 
 const char* aux_kernel_name(const Handle* h) {
     if (h->generic) return h->gossip ? "" : "k_scan_* + k_ps_push_fill";
     if (!h->g.has_link || fused_marks(h)) return "";
-    if (h->sharded) return h->gossip ? "k_gs_link_scatter_x" : "";
+    if (h->sharded) return h->gossip ? "k_gs_link_scatter_x" : "k_ps_link_scatter_x";
     return "k_link_count";
 }
 
@@ -531,8 +529,6 @@ void launch_main(Handle* h, int64_t k, const Xchg* x) {
         }
     } else if (h->generic) {
         launch_ps_push_emit(a, l);
-    } else if (x && h->g.has_link) {
-        launch_ps_pull_x(a, *x, l);
     } else {
         launch_ps_pull(a, l);
     }
@@ -554,8 +550,9 @@ int launch_aux(Handle* h, int64_t k, const Xchg* x) {
         const int c = (int)(r & 1u);
         launch_exclusive_scan(h->bcnt[c], h->boff[c], h->g.actors, h->scan_scratch, h->stream);
         launch_ps_push_fill(a, h->slot[c], h->boff[c], l);
-    } else if (h->g.has_link && !fused_marks(h)) {
-        launch_link_count(a, l);
+    } else if (h->g.has_link) {
+        if (x) launch_ps_link_scatter_x(a, *x, l);
+        else if (!fused_marks(h)) launch_link_count(a, l);
     }
     return GP_OK;
 }

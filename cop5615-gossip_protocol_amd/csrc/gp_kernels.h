@@ -15,10 +15,6 @@ constexpr int kMaxGrid = 256 * GP_GRID_PER_CU;
 #ifndef GP_PS_WAVES
 #define GP_PS_WAVES 6
 #endif
-// Waves per SIMD of the sharded round kernel that also writes the exchange entries (k_ps_pull_x).
-#ifndef GP_PSX_WAVES
-#define GP_PSX_WAVES 5
-#endif
 constexpr int kParts = 64;          // completion sub-counters per round (one 64 B line each)
 constexpr int kPartStride = 16;     // u32 words between sub-counters
 constexpr int kPartRing = 4;        // rounds kept in the sub-counter ring
@@ -182,6 +178,13 @@ struct Launch {
 int grid_for(uint32_t n);
 uint32_t span_for(uint32_t n, int grid);
 
+// The one-GPU quiet-wave push-sum round on 3D grids walks y-slabs (k_ps_slab<LM>, GP_SLAB).
+#ifndef GP_SLAB
+#define GP_SLAB 0
+#endif
+constexpr bool kSlabWalk = GP_SLAB != 0;
+inline bool ps_slab_walk(const RoundArgs& a) { return kSlabWalk && a.act_cur != nullptr && a.g.gz > 1; }
+
 // round kernels
 void launch_ps_pull(const RoundArgs& a, const Launch& l);
 void launch_gs_pull(const RoundArgs& a, const Launch& l);
@@ -195,8 +198,7 @@ void launch_ps_push_fill(const RoundArgs& a, uint32_t* slot_cur, const uint32_t*
 void launch_gs_push(const RoundArgs& a, const Launch& l);
 void launch_gs_full4(const RoundArgs& a, const Launch& l);  // full gossip, one GPU (lo == 0)
 // sharded variants: remote link / full-topology messages go to the send chunks of x
-// sharded Imp3D push-sum round that also fills the send chunks with its remote link messages
-void launch_ps_pull_x(const RoundArgs& a, const Xchg& x, const Launch& l);
+void launch_ps_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);
 void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);
 void launch_gs_push_x(const RoundArgs& a, const Xchg& x, const Launch& l);
 // halo faces of F(k) into the send chunks of rank +-1: direction bytes, crossing push-sum messages

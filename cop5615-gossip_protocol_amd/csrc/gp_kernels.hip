@@ -190,27 +190,24 @@ constexpr uint32_t kLinkUnroll = GP_LINK_UNROLL;
 // instruction mix stays: bit 6 held row, 7 the six neighbours' direction bytes, 8 flags, 9 CSR
 // offsets (li = v, nl = 1 instead), 10 CSR sources, 11 link marks, 12 lpos, 13 fired-link
 // message gathers, 14 grid-hit message gathers, 15 only the +-G^2 grid-hit gathers, 16 only the
-// +-G^2 direction bytes; shards: 17 no exchange entries staged, 18 no Philox redraw of remote
-// link sources.
+// +-G^2 direction bytes.
 #ifndef GP_ABLATE
 #define GP_ABLATE 0
 #endif
 constexpr uint32_t kAblate = GP_ABLATE;
+// A/B knob: cap the round kernel's SGPRs (GP_PS_SGPR, 0 = the compiler's choice).  A 256-thread
+// workgroup is admitted per CU only while 800 / (ceil(sgpr / 16) * 16 + 16) allows it
+// (MI355X_MICROARCH.md, residency): 106 SGPRs -> 6 workgroups, <= 96 -> 7, <= 80 -> 8.
+#if defined(GP_PS_SGPR) && GP_PS_SGPR > 0
+#define GP_PS_SGPR_ATTR __attribute__((amdgpu_num_sgpr(GP_PS_SGPR)))
+#else
+#define GP_PS_SGPR_ATTR
+#endif
+
 template <uint32_t BIT>
 __device__ __forceinline__ uint32_t ab(uint32_t i) {
     return (kAblate & BIT) ? (i & 0xFFFu) : i;
 }
-
-// Whether u's round-r push-sum draw took its extra link (the draw of ps_finish, recomputed).
-__device__ __forceinline__ bool link_drawn(const Geom& g, uint64_t seed, uint32_t u, uint32_t r) {
-    if (kAblate & 262144u) return (u & 7u) == 0u;  // timing only: no redraw
-    const uint32_t m = presence(g, u);
-    return kth_bit(m, scale_draw(philox_x(u, r, kStreamPush, seed), popc(m))) == kDirLink;
-}
-
-// A shard's link entry for a source whose draw took the link but that sent nothing carries
-// W = -1 (a real message's W is never negative: sums and halvings of W_i = 1, program.fs:78).
-__device__ __forceinline__ bool sent_nothing(double2 m) { return __double_as_longlong(m.y) < 0; }
 // A/B knob: the message as one 16-byte non-temporal store (1) or two 8-byte ones (0).
 #ifndef GP_NT16
 #define GP_NT16 0
@@ -307,18 +304,9 @@ __device__ __forceinline__ PsLevel1 ps_level1(const RoundArgs& a, const Geom& g,
     return p;
 }
 
-// A sharded round's link message whose CSR slot another rank owns (LM == 2): the global slot
-// (kNoSlot: none) and the message, staged by the caller into that rank's send chunk.
-constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
-struct RemoteLink {
-    uint32_t slo, shi;  // this rank's link slots (in)
-    uint32_t slot;      // out: kNoSlot or the remote slot
-    double2 msg;
-};
-
 template <int LM, bool PRE = false>
 __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
-                                              const PsLevel1& p, bool mark, RemoteLink* rl = nullptr) {
+                                              const PsLevel1& p, bool mark) {
     const uint32_t m = p.m;
     if (!m) return 0;
     const uint32_t code = (kAblate & 8u) ? kth_bit(m, v % popc(m))
@@ -398,17 +386,12 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
             uint8_t lc[kLinkUnroll];
 #pragma unroll
             for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, ab<2048u>(li + k), a.slot_lo);
-            // ---- level 3: the messages of the sources whose slot is marked.  Shards: a remote
-            // source's slot carries no mark; the source's round r-1 direction (Philox, as its own
-            // rank drew it) says whether its message took the link, and its rank then sent the slot
-            // an entry in that round (a negative W: it had nothing to send, program.fs:125-127).
+            // ---- level 3: the messages of the sources whose slot is marked
 #pragma unroll
             for (uint32_t k = 0; k < kLinkUnroll; ++k) {
-                const bool remote = LM == 2 && (ls[k] < a.lo || ls[k] >= a.hi);
-                lk[k] = k < nl && (remote ? link_drawn(g, a.seed, ls[k], r - 1u) : lc[k] == a.tag_prev);
-                if (LM == 2 && remote) {
-                    lm[k] = lk[k] ? a.rmsg_prev[li + k] : make_double2(0.0, 0.0);
-                    lk[k] = lk[k] && !sent_nothing(lm[k]);
+                lk[k] = k < nl && lc[k] == a.tag_prev;  // round-tagged marks: nothing to clear
+                if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
+                    lm[k] = a.rmsg_prev[li + k];
                 } else {
                     lm[k] = load_sel(a.msg_prev, lk[k], ab<8192u>(ls[k]), v);
                 }
@@ -420,18 +403,10 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                     add(lm[k]);
                 }
             for (uint32_t k = kLinkUnroll; k < nl; ++k) {  // rare: more than kLinkUnroll sources
-                const uint32_t u = a.rev_src[li + k];
-                if (LM == 2 && (u < a.lo || u >= a.hi)) {
-                    if (link_drawn(g, a.seed, u, r - 1u)) {
-                        const double2 mm = a.rmsg_prev[li + k];
-                        if (!sent_nothing(mm)) {
-                            flush(u);
-                            add(mm);
-                        }
-                    }
-                } else if (a.lcnt_prev[li + k] == a.tag_prev) {
+                if (a.lcnt_prev[li + k] == a.tag_prev) {
+                    const uint32_t u = a.rev_src[li + k];
                     flush(u);
-                    add(a.msg_prev[u]);
+                    add(LM == 2 && (u < a.lo || u >= a.hi) ? a.rmsg_prev[li + k] : a.msg_prev[u]);
                 }
             }
         }
@@ -453,18 +428,6 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
     __builtin_nontemporal_store(o.send ? (uint8_t)code : kDirNone, &a.dir_cur[v]);
     if constexpr (LM == 1 && kFuseLinkMarks) {  // the link pass's mark, written by the sender
         if (o.send && code == kDirLink) a.lcnt_cur[a.lpos[ab<4096u>(v)]] = (uint8_t)a.tag_cur;
-    }
-    if constexpr (LM == 2) {  // shards: a local slot gets the mark, a remote one an exchange entry
-        // (always, when the draw took the link: the receiver knows the draw, not whether v sent)
-        if (rl && code == kDirLink && v < g.wired) {
-            const uint32_t lp = a.lpos[v];
-            if (lp >= rl->slo && lp < rl->shi) {
-                if (o.send) a.lcnt_cur[lp] = (uint8_t)a.tag_cur;
-            } else {
-                rl->slot = lp;
-                rl->msg = o.send ? o.msg : make_double2(0.0, -1.0);
-            }
-        }
     }
     if (f != f0) a.flags[v] = f;
     if (o.conv_now) a.frozen[v] = o.msg;
@@ -490,7 +453,7 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
 // its direction bytes become kDirNone and nothing else changes.
 // Q: quiet-wave marks allocated (a.act_cur != null); the small graphs run without (Q = false).
 template <int LM, bool Q>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WAVES))) void k_ps_pull(RoundArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WAVES))) GP_PS_SGPR_ATTR void k_ps_pull(RoundArgs a) {
     const Geom g = a.g;
     const uint32_t r = a.r;
     uint32_t newly = 0;
@@ -787,139 +750,42 @@ __device__ __forceinline__ void put(const Xchg& x, uint32_t q, uint32_t pos, uin
 // block-level reservations (three barriers and one global atomic per peer each).
 constexpr uint32_t kShardPer = 4;
 
-// Sharded push-sum round (LM == 2) with its exchange entries: the round kernel itself marks the
-// local link slots of its messages (as on one GPU) and appends a message whose CSR slot another
-// rank owns to that rank's send chunk as (global slot, s, w).  Entries collect per wave and peer
-// in LDS and go out kStageCap at a time: one reservation atomic per flush and one coalesced run
-// of slots and messages (a separate scatter pass re-read direction bytes, lpos and messages and
-// reserved per block of 1024 actors: 0.65 ms per round at 125M actors per rank).
-constexpr uint32_t kStageCap = 32;
-
-struct WaveStage {
-    double2* msg;    // [world][kStageCap]
-    uint32_t* slot;  // [world][kStageCap]
-    uint32_t* cnt;   // [world] entries buffered per peer
-};
-
-__host__ __device__ constexpr size_t stage_lds_bytes(uint32_t world) {
-    return (size_t)(kBlock / 64) * world * (kStageCap * (sizeof(double2) + sizeof(uint32_t)) + sizeof(uint32_t));
-}
-
-__device__ __forceinline__ WaveStage wave_stage(uint32_t world) {
-    extern __shared__ __align__(16) unsigned char stage_lds[];
-    const uint32_t w = threadIdx.x >> 6, nw = kBlock / 64;
-    const size_t per = (size_t)world * kStageCap;
-    WaveStage st;
-    st.msg = reinterpret_cast<double2*>(stage_lds) + w * per;
-    st.slot = reinterpret_cast<uint32_t*>(stage_lds + nw * per * sizeof(double2)) + w * per;
-    st.cnt = reinterpret_cast<uint32_t*>(stage_lds + nw * per * (sizeof(double2) + sizeof(uint32_t))) + w * world;
-    return st;
-}
-
-__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// The wave's n buffered entries of peer q into a reserved run of q's sub-segment (all lanes).
-__device__ __forceinline__ void stage_flush(const Xchg& x, const WaveStage& st, uint32_t q, uint32_t n) {
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(ctr_at(x, q, my_sub()), n);
-    base = (uint32_t)__shfl((int)base, 0, 64);
-    if (lane < n) put<true>(x, q, base + lane, st.slot[q * kStageCap + lane], st.msg[q * kStageCap + lane]);
-}
-
-#ifndef GP_STAGE
-#define GP_STAGE 2
-#endif
-// Every lane of the wave calls it: rl.slot != kNoSlot lanes append (slot, msg) for its owner rank.
-// GP_STAGE 2: one LDS atomic per entry takes its buffer position; an entry past a full buffer goes
-// straight to the chunk with its own reservation, and full buffers are flushed after the round.
-__device__ __forceinline__ void stage_add2(const Xchg& x, const WaveStage& st, const RemoteLink& rl) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const bool want = rl.slot != kNoSlot;
-    if (!__ballot(want)) return;  // wave-uniform
-    if (want) {
-        const uint32_t q = owner(x.sbnd, x.world, rl.slot);
-        const uint32_t pos = atomicAdd(&st.cnt[q], 1u);  // LDS
-        if (pos < kStageCap) {
-            st.slot[q * kStageCap + pos] = rl.slot;
-            st.msg[q * kStageCap + pos] = rl.msg;
-        } else {
-            put<true>(x, q, atomicAdd(ctr_at(x, q, my_sub()), 1u), rl.slot, rl.msg);
-        }
+// Sharded push-sum link pass: a link message whose CSR slot is this rank's gets the slot's link
+// count (the receiver reads msg_prev[u] itself, as on one GPU); one whose slot belongs to another
+// rank goes to that rank's send chunk as (global slot, s, w), written into the same slot there.
+__global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg x) {
+    if (applied_converged(a)) return;  // block-uniform: F(r) was a no-op
+    const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
+    const uint32_t base = a.lo + blockIdx.x * kBlock * kShardPer + threadIdx.x;
+    const uint32_t slo = x.sbnd[x.rank], shi = x.sbnd[x.rank + 1];
+    bool l[kShardPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kShardPer; ++j) {
+        const uint32_t u = base + j * kBlock;
+        l[j] = u < n && load_sel(a.dir_cur, u < n, u, a.lo) == kDirLink;
     }
-    const uint32_t c = lane < x.world ? st.cnt[lane] : 0u;
-    uint64_t full = __ballot(c >= kStageCap);
-    while (full) {  // wave-uniform
-        const uint32_t qq = (uint32_t)__builtin_ctzll(full);
-        full &= full - 1u;
-        stage_flush(x, st, qq, kStageCap);
-        if (lane == 0) st.cnt[qq] = 0u;
+    uint32_t lp[kShardPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kShardPer; ++j) lp[j] = load_sel(a.lpos, l[j], base + j * kBlock, a.lo);
+    // only a remote link needs its message: the fired ~1/7 of senders would otherwise pull in
+    // ~70% of msg_cur's lines (8 messages per 128 B line)
+    bool rm[kShardPer];
+    double2 mm[kShardPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kShardPer; ++j) {
+        rm[j] = l[j] && (lp[j] < slo || lp[j] >= shi);
+        mm[j] = load_sel(a.msg_cur, rm[j], base + j * kBlock, a.lo);
     }
-}
-
-__device__ __forceinline__ void stage_add(const Xchg& x, const WaveStage& st, const RemoteLink& rl) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const bool want = rl.slot != kNoSlot;
-    const uint32_t q = want ? owner(x.sbnd, x.world, rl.slot) : 0u;
-    uint64_t rem = __ballot(want);
-    while (rem) {  // wave-uniform: one pass per peer present in this wave's entries
-        const uint32_t qq = (uint32_t)__shfl((int)q, (int)__builtin_ctzll(rem), 64);
-        const bool mine = want && q == qq;
-        const uint64_t mask = __ballot(mine);
-        rem &= ~mask;
-        const uint32_t c = (uint32_t)__popcll(mask);
-        uint32_t n = st.cnt[qq];
-        if (n + c > kStageCap) {
-            stage_flush(x, st, qq, n);
-            n = 0;
-        }
-        if (c <= kStageCap) {
-            if (mine) {
-                const uint32_t pos = qq * kStageCap + n + mbcnt64(mask);
-                st.slot[pos] = rl.slot;
-                st.msg[pos] = rl.msg;
-            }
-            n += c;
-        } else {  // more than a buffer from one wave (rare): straight to the chunk
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(ctr_at(x, qq, my_sub()), c);
-            base = (uint32_t)__shfl((int)base, 0, 64);
-            if (mine) put<true>(x, qq, base + mbcnt64(mask), rl.slot, rl.msg);
-        }
-        if (lane == 0) st.cnt[qq] = n;
+    uint32_t q[kShardPer], pos[kShardPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kShardPer; ++j) {
+        if (l[j] && !rm[j]) a.lcnt_cur[lp[j]] = (uint8_t)a.tag_cur;
+        q[j] = rm[j] ? owner(x.sbnd, x.world, lp[j]) : 0u;
     }
-}
-
-template <int LM>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PSX_WAVES))) void k_ps_pull_x(RoundArgs a,
-                                                                                                          Xchg x) {
-    static_assert(LM == 2, "the exchange-writing round kernel is the sharded Imp3D one");
-    const Geom g = a.g;
-    const uint32_t r = a.r;
-    uint32_t newly = 0;
-    uint32_t v, end, step;
-    node_range(a.lo, a.hi, a.span, v, end, step);
-    if (gate_count(a, a.r) >= a.target) return;  // block-uniform
-    const WaveStage st = wave_stage(x.world);
-    const uint32_t lane = threadIdx.x & 63u;
-    if (lane < x.world) st.cnt[lane] = 0u;
-    RemoteLink rl;
-    rl.slo = x.sbnd[x.rank];
-    rl.shi = x.sbnd[x.rank + 1];
-    for (; v - lane < end; v += step) {  // wave-uniform trip count: every lane reaches stage_add
-        rl.slot = kNoSlot;
-        if (v < end) newly += ps_finish<LM>(a, g, r, v, ps_level1<LM>(a, g, r, v), false, &rl);
-        if (kAblate & 131072u) continue;  // timing only: entries not written
-        if (GP_STAGE == 2) stage_add2(x, st, rl);
-        else stage_add(x, st, rl);
-    }
-    for (uint32_t q = 0; q < x.world; ++q) {
-        const uint32_t n = st.cnt[q];
-        if (n) stage_flush(x, st, q, n);
-    }
-    block_add(newly, a.parts, r);
+    block_reserve(x, rm, q, pos);
+#pragma unroll
+    for (uint32_t j = 0; j < kShardPer; ++j)
+        if (rm[j]) put<true>(x, q[j], pos[j], lp[j], mm[j]);
 }
 
 __global__ __launch_bounds__(kBlock) void k_gs_link_scatter_x(RoundArgs a, Xchg x) {
@@ -1104,7 +970,10 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
             }
             if (full) atomicAdd(&a.inc_cur[t], 1u);
             else if (gossip) a.lcnt_cur[t] = (uint8_t)((e >> 31) + 1u);
-            else a.rmsg_cur[t] = in.msg[i];  // the slot's message (no mark: k_ps_pull_x redraws)
+            else {  // the sender's message into the receiver's slot, the slot marked
+                a.rmsg_cur[t] = in.msg[i];
+                a.lcnt_cur[t] = (uint8_t)a.tag_cur;
+            }
         }
     }
 }
@@ -1576,12 +1445,6 @@ uint32_t span_for(uint32_t n, int grid) {
     return (s + kBlock - 1) / kBlock * kBlock;
 }
 
-// The one-GPU quiet-wave round kernel on 3D grids walks y-slabs (k_ps_slab<LM>).
-#ifndef GP_SLAB
-#define GP_SLAB 0
-#endif
-constexpr bool kSlabWalk = GP_SLAB != 0;
-
 // Dynamic LDS per workgroup that caps the round kernel's residency (A/B knob): 24 KB allows 6
 // workgroups (= 6 waves per SIMD) per CU's 160 KB whatever the VGPR count permits.
 #ifndef GP_PS_LDS_CAP
@@ -1592,10 +1455,12 @@ void launch_ps_pull(const RoundArgs& a, const Launch& l) {
     const unsigned lds = GP_PS_LDS_CAP;
     const bool q = a.act_cur != nullptr;
     if (!a.g.has_link) {
-        if (q && kSlabWalk && a.g.gz > 1) hipLaunchKernelGGL((k_ps_slab<0>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
+        if (ps_slab_walk(a)) hipLaunchKernelGGL((k_ps_slab<0>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
         else if (q) hipLaunchKernelGGL((k_ps_pull<0, true>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
         else hipLaunchKernelGGL((k_ps_pull<0, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
-    } else if (q && kSlabWalk && a.g.gz > 1) {
+    } else if (a.rmsg_prev) {
+        hipLaunchKernelGGL((k_ps_pull<2, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
+    } else if (ps_slab_walk(a)) {
         hipLaunchKernelGGL((k_ps_slab<1>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
     } else if (q) {
         hipLaunchKernelGGL((k_ps_pull<1, true>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
@@ -1639,8 +1504,8 @@ static unsigned scatter_blocks(const RoundArgs& a) {
     return n > a.lo ? (n - a.lo + kShardPer * kBlock - 1) / (kShardPer * kBlock) : 0u;
 }
 
-void launch_ps_pull_x(const RoundArgs& a, const Xchg& x, const Launch& l) {
-    hipLaunchKernelGGL((k_ps_pull_x<2>), dim3(l.grid), dim3(kBlock), (unsigned)stage_lds_bytes(x.world), l.stream, a, x);
+void launch_ps_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l) {
+    if (const unsigned b = scatter_blocks(a)) hipLaunchKernelGGL(k_ps_link_scatter_x, dim3(b), dim3(kBlock), 0, l.stream, a, x);
 }
 
 void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l) {
