@@ -388,8 +388,8 @@ int ensure_trace(Handle* h, int64_t need) {
     return GP_OK;
 }
 
-// Quiet-wave marks: one byte per 64 actors.
-size_t act_bytes(const Handle* h) { return (size_t)(h->g.actors + 63u) / 64u + 1u; }
+// Quiet-wave marks: one byte per segment of kActSeg actors.
+size_t act_bytes(const Handle* h) { return (size_t)(h->g.actors + kActSeg - 1u) / kActSeg + 1u; }
 
 int reset(Handle* h) {
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -469,9 +469,8 @@ const char* round_kernel_name(const Handle* h) {
     if (h->gossip) return "k_gs_push";
     if (h->generic) return "k_ps_push_emit";
     if (h->sharded && h->g.has_link) return h->rmsg[0] ? "k_ps_pull<2, false>" : "k_ps_pull<1, false>";
-    const bool slab = ps_slab_walk(h->args(0));
-    if (h->g.has_link) return slab ? "k_ps_slab<1>" : h->act[0] ? "k_ps_pull<1, true>" : "k_ps_pull<1, false>";
-    return slab ? "k_ps_slab<0>" : h->act[0] ? "k_ps_pull<0, true>" : "k_ps_pull<0, false>";
+    if (h->g.has_link) return h->act[0] ? "k_ps_quiet<1>" : "k_ps_pull<1, false>";
+    return h->act[0] ? "k_ps_quiet<0>" : "k_ps_pull<0, false>";
 }
 
 const char* aux_kernel_name(const Handle* h) {

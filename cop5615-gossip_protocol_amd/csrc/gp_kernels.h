@@ -178,12 +178,13 @@ struct Launch {
 int grid_for(uint32_t n);
 uint32_t span_for(uint32_t n, int grid);
 
-// The one-GPU quiet-wave push-sum round on 3D grids walks y-slabs (k_ps_slab<LM>, GP_SLAB).
-#ifndef GP_SLAB
-#define GP_SLAB 0
+// Quiet-wave marks: one byte per segment of kActSeg actors (GP_ACT_SEG: 16, or 64 = one wave).
+#ifndef GP_ACT_SEG
+#define GP_ACT_SEG 16
 #endif
-constexpr bool kSlabWalk = GP_SLAB != 0;
-inline bool ps_slab_walk(const RoundArgs& a) { return kSlabWalk && a.act_cur != nullptr && a.g.gz > 1; }
+constexpr uint32_t kActSeg = GP_ACT_SEG;
+constexpr uint32_t kActShift = kActSeg == 64u ? 6u : kActSeg == 32u ? 5u : kActSeg == 16u ? 4u : 3u;
+static_assert((1u << kActShift) == kActSeg, "GP_ACT_SEG: 8, 16, 32 or 64");
 
 // round kernels
 void launch_ps_pull(const RoundArgs& a, const Launch& l);

@@ -195,18 +195,29 @@ constexpr uint32_t kLinkUnroll = GP_LINK_UNROLL;
 #define GP_ABLATE 0
 #endif
 constexpr uint32_t kAblate = GP_ABLATE;
-// A/B knob: cap the round kernel's SGPRs (GP_PS_SGPR, 0 = the compiler's choice).  A 256-thread
+// The quiet-wave round kernel's SGPR cap (GP_PSQ_SGPR, 0 = the compiler's choice).  A 256-thread
 // workgroup is admitted per CU only while 800 / (ceil(sgpr / 16) * 16 + 16) allows it
 // (MI355X_MICROARCH.md, residency): 106 SGPRs -> 6 workgroups, <= 96 -> 7, <= 80 -> 8.
-#if defined(GP_PS_SGPR) && GP_PS_SGPR > 0
-#define GP_PS_SGPR_ATTR __attribute__((amdgpu_num_sgpr(GP_PS_SGPR)))
+#ifndef GP_PSQ_SGPR
+#define GP_PSQ_SGPR 96
+#endif
+#ifndef GP_PSQ_WAVES
+#define GP_PSQ_WAVES 7
+#endif
+#if GP_PSQ_SGPR > 0
+#define GP_PSQ_SGPR_ATTR __attribute__((amdgpu_num_sgpr(GP_PSQ_SGPR)))
 #else
-#define GP_PS_SGPR_ATTR
+#define GP_PSQ_SGPR_ATTR
 #endif
 
 template <uint32_t BIT>
 __device__ __forceinline__ uint32_t ab(uint32_t i) {
     return (kAblate & BIT) ? (i & 0xFFFu) : i;
+}
+
+// Lanes below this one whose bit is set in m.
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 // A/B knob: the message as one 16-byte non-temporal store (1) or two 8-byte ones (0).
 #ifndef GP_NT16
@@ -433,8 +444,8 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
     if (o.conv_now) a.frozen[v] = o.msg;
     if (mark) {  // the waves with work in round r + 1: v's own if it still updates, its target's
         const uint8_t t = (uint8_t)link_tag(r + 1u);
-        if (!(f & 16u)) a.act_cur[v >> 6] = t;
-        if (o.send) a.act_cur[dir_target(g, v, code, code == kDirLink ? link_of(a.seed, v, a.nodes) : 0u) >> 6] = t;
+        if (!(f & 16u)) a.act_cur[v >> kActShift] = t;
+        if (o.send) a.act_cur[dir_target(g, v, code, code == kDirLink ? link_of(a.seed, v, a.nodes) : 0u) >> kActShift] = t;
     }
     return o.conv_now ? 1u : 0u;
 }
@@ -445,6 +456,74 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
     return ps_finish<LM>(a, g, r, v, ps_level1<LM>(a, g, r, v), mark);
 }
 
+// The quiet-wave tail with compaction.  Marks are per segment of kActSeg actors: F(r) marks the
+// segment of every actor that still updates and of every message's target.  In F(r + 1) a wave
+// reads the marks of 64 consecutive segments (its XCD group's span, grid-stride), writes "send
+// nothing" (kDirNone) into the direction bytes of the unmarked ones — they hold only converged
+// actors and receive nothing, so that is their whole round — and then walks the marked
+// segments only, 64 / kActSeg of them per pass of its 64 lanes (each segment's actors stay
+// contiguous in a lane group, so the loads keep their coalescing).  With 64-actor marks nearly
+// every wave of the tail had work (86% at 3% active actors); 16-actor segments skip ~60%.
+// One walk loop with one ps_actor call serves both the dense rounds and the tail (two inlined
+// copies of the actor body cost 4 spilled VGPRs and a wave per SIMD).
+// Walk state of the compacted tail (per wave): the next 64-segment chunk of the XCD group's span,
+// the marked segments of the current chunk (in LDS) and how many of them are walked.
+struct TailWalk {
+    uint32_t base, s1, stride, c, k;
+    uint32_t* list;
+};
+
+__device__ __forceinline__ TailWalk tail_walk(const RoundArgs& a) {
+    __shared__ uint32_t seg_list[kBlock];
+    TailWalk t;
+    const uint32_t nseg = (a.hi + kActSeg - 1u) >> kActShift;  // one GPU: actors [0, hi)
+    const uint32_t grp = blockIdx.x & 7u, wpg = (gridDim.x >> 3) * (kBlock / 64u);
+    const uint32_t wid = (blockIdx.x >> 3) * (kBlock / 64u) + (threadIdx.x >> 6);
+    const uint32_t sspan = ((nseg + 7u) / 8u + 63u) / 64u * 64u;
+    const uint32_t s0 = grp * sspan;
+    t.s1 = s0 + sspan < nseg ? s0 + sspan : nseg;
+    t.base = s0 + wid * 64u;
+    t.stride = wpg * 64u;
+    t.c = t.k = 0;
+    t.list = seg_list + (threadIdx.x & ~63u);
+    return t;
+}
+
+// The next actor of this lane in the compacted tail walk (a.hi: none this pass); false when the
+// wave's span is done.  Wave-uniform.  A chunk's unmarked segments get "send nothing"
+// (kDirNone) direction bytes as the chunk is opened.
+__device__ __forceinline__ bool tail_next(const RoundArgs& a, TailWalk& t, uint8_t tag, uint32_t& v) {
+    constexpr uint32_t S = kActSeg, PER = 64u / kActSeg;
+    const uint32_t lane = threadIdx.x & 63u;
+    while (t.k >= t.c) {
+        if (t.base >= t.s1) return false;
+        const uint32_t seg = t.base + lane;
+        const bool valid = seg < t.s1;
+        const bool act = valid && a.act_prev[seg] == tag;
+        if (valid && !act) {  // kActSeg direction bytes (the array is padded past the last actor)
+            uint8_t* d = a.dir_cur + (size_t)seg * S;
+            if constexpr (S == 16u) {
+                typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+                static_assert(kDirNone == 7, "kDirNone bytes");
+                const u4 none = {0x07070707u, 0x07070707u, 0x07070707u, 0x07070707u};
+                __builtin_nontemporal_store(none, reinterpret_cast<u4*>(d));
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < S; ++i) __builtin_nontemporal_store(kDirNone, d + i);
+            }
+        }
+        const uint64_t m = __ballot(act);
+        if (act) t.list[mbcnt64(m)] = seg;
+        t.c = (uint32_t)__popcll(m);
+        t.k = 0;
+        t.base += t.stride;
+    }
+    const uint32_t j = t.k + lane / S;
+    v = j < t.c ? t.list[j] * S + lane % S : a.hi;
+    t.k += PER;
+    return true;
+}
+
 // Grid-stride over the XCD-aware node range (a z-march walk, each workgroup carrying a tile up
 // through the planes so the +-G^2 rows come from L2, read 10% fewer lines but ran 12-20%
 // slower: DESIGN.md §8).
@@ -453,7 +532,7 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
 // its direction bytes become kDirNone and nothing else changes.
 // Q: quiet-wave marks allocated (a.act_cur != null); the small graphs run without (Q = false).
 template <int LM, bool Q>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WAVES))) GP_PS_SGPR_ATTR void k_ps_pull(RoundArgs a) {
+__device__ __forceinline__ void ps_pull_body(const RoundArgs& a) {
     const Geom g = a.g;
     const uint32_t r = a.r;
     uint32_t newly = 0;
@@ -490,8 +569,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WA
     const bool mark = Q && prev >= a.act_thr;                          // F(r) marks round r + 1
     const bool skip = Q && r >= 2u && a.total[r - 2] >= a.act_thr;  // F(r - 1) marked round r
     const uint8_t tag = (uint8_t)a.tag_cur;  // link_tag(r)
+    if constexpr (Q && kActSeg < 64u) {
+        TailWalk t = tail_walk(a);
+        const bool tail = skip;  // block-uniform: the compacted segment walk of the run's tail
+        for (;;) {
+            uint32_t u;
+            if (tail) {
+                if (!tail_next(a, t, tag, u)) break;
+            } else {
+                if (v >= end) break;
+                u = v;
+                v += step;
+            }
+            if (u < a.hi) newly += ps_actor<LM>(a, g, r, u, mark);
+        }
+        block_add(newly, a.parts, r);
+        return;
+    }
     for (; v < end; v += step) {
-        if (skip && a.act_prev[v >> 6] != tag) {  // wave-uniform: 64 consecutive actors
+        if (skip && a.act_prev[v >> kActShift] != tag) {  // wave-uniform: 64 consecutive actors
             __builtin_nontemporal_store(kDirNone, &a.dir_cur[v]);
             continue;
         }
@@ -500,43 +596,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WA
     block_add(newly, a.parts, r);
 }
 
-// k_ps_slab: the one-GPU quiet-wave round kernel (k_ps_pull<LM, true>) on 3D grids with another
-// walk: XCD group s = blockIdx % 8 takes the rows y in [s*G/8, (s+1)*G/8) of every z-plane and
-// walks them z-major, so the +-G^2 neighbours of an
-// actor are one slab-plane (G/8 rows) away in the walk instead of a whole plane: their message and
-// direction rows are still in the XCD's L2 when they are read (the node-range walk re-fetched them
-// from HBM: 2.1M of 5.4M read lines per round at 10M actors, profiles/round3/ablation).
-template <int LM>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WAVES))) void k_ps_slab(RoundArgs a) {
-    const Geom g = a.g;
-    const uint32_t r = a.r;
-    uint32_t newly = 0;
-    {
-        const unsigned long long prev = gate_count(a, a.r);
-        if (prev >= a.target) return;
-        const bool mark = prev >= a.act_thr;
-        const bool skip = r >= 2u && a.total[r - 2] >= a.act_thr;
-        const uint8_t tag = (uint8_t)a.tag_cur;
-        const uint32_t s = blockIdx.x & 7u, j = blockIdx.x >> 3, per = gridDim.x >> 3;
-        const uint32_t y0 = s * g.gy / 8u, y1 = (s + 1u) * g.gy / 8u;
-        const uint32_t sp = (y1 - y0) * g.gx;  // actors of one slab-plane
-        const uint32_t n = g.gz * sp;
-        const FastDiv dsp = make_fastdiv(sp ? sp : 1u);
-        for (uint32_t i = j * kBlock + threadIdx.x; i < n; i += per * kBlock) {
-            const uint32_t z = fdiv(i, dsp), rem = i - z * sp;
-            const uint32_t yy = fdiv(rem, g.dx);
-            const uint32_t u = z * g.plane + (y0 + yy) * g.gx + (rem - yy * g.gx);
-            if (u >= g.wired) continue;  // the partial last plane; the isolated actor has no work
-            if (skip && a.act_prev[u >> 6] != tag) {
-                __builtin_nontemporal_store(kDirNone, &a.dir_cur[u]);
-                continue;
-            }
-            newly += ps_actor<LM>(a, g, r, u, mark);
-        }
-        block_add(newly, a.parts, r);
-    }
+template <int LM, bool Q>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS_WAVES))) void k_ps_pull(RoundArgs a) {
+    ps_pull_body<LM, Q>(a);
 }
 
+// The one-GPU round kernel of large graphs (quiet waves: from 2^20 actors).  Its SGPRs are capped
+// (GP_PSQ_SGPR) so that seven 256-thread workgroups fit a CU (106 SGPRs admit six: MI355X
+// residency rule 800 / (ceil(sgpr / 16) * 16 + 16)), and it runs on a grid of exactly the
+// resident workgroups (quiet_grid): every workgroup of an XCD sweeps its span together.
+// C3 -4.0%, 100M -2% against 6 per CU on a 16-per-CU grid (profiles/round3/occupancy_ab).
+template <int LM>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PSQ_WAVES))) GP_PSQ_SGPR_ATTR void k_ps_quiet(
+    RoundArgs a) {
+    ps_pull_body<LM, true>(a);
+}
 
 // ------------------------------------------------------------------ gossip, grid topologies
 // dir byte = chain-0 code | chain-1 code << 4 (15 = no chain)
@@ -1451,19 +1525,23 @@ uint32_t span_for(uint32_t n, int grid) {
 #define GP_PS_LDS_CAP 0
 #endif
 
+// The quiet-wave kernel's grid: the workgroups resident at once (GP_PSQ_PER_CU per CU; 7 with the
+// SGPR cap), unless the node range needs fewer.
+#ifndef GP_PSQ_PER_CU
+#define GP_PSQ_PER_CU 7
+#endif
+static int quiet_grid(const Launch& l) { return l.grid < 256 * GP_PSQ_PER_CU ? l.grid : 256 * GP_PSQ_PER_CU; }
+
 void launch_ps_pull(const RoundArgs& a, const Launch& l) {
     const unsigned lds = GP_PS_LDS_CAP;
     const bool q = a.act_cur != nullptr;
     if (!a.g.has_link) {
-        if (ps_slab_walk(a)) hipLaunchKernelGGL((k_ps_slab<0>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
-        else if (q) hipLaunchKernelGGL((k_ps_pull<0, true>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
+        if (q) hipLaunchKernelGGL((k_ps_quiet<0>), dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a);
         else hipLaunchKernelGGL((k_ps_pull<0, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
     } else if (a.rmsg_prev) {
         hipLaunchKernelGGL((k_ps_pull<2, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
-    } else if (ps_slab_walk(a)) {
-        hipLaunchKernelGGL((k_ps_slab<1>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
     } else if (q) {
-        hipLaunchKernelGGL((k_ps_pull<1, true>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
+        hipLaunchKernelGGL((k_ps_quiet<1>), dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a);
     } else {
         hipLaunchKernelGGL((k_ps_pull<1, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
     }

@@ -66,7 +66,7 @@ case $MODE in
       ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_$c" -o p -- python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-1000000} ${PROF_ARGS} > "$O/pmc_$c.log" 2>&1 )
       rc=$?; echo "pmc $c rc=$rc"; tail -1 "$O/pmc_$c.log"; [ $rc -eq 0 ] || exit $rc
     done
-    python3 "$R/tools/pmc_run_summary.py" "$O/pmc_FETCH_SIZE" "$O/pmc_WRITE_SIZE" "$O/pmc_run.json" "${PMC_WORKLOAD:-10000000 Imp3D push-sum}" "${PMC_KERNEL:-k_ps_pull<1, true>}" ;;
+    python3 "$R/tools/pmc_run_summary.py" "$O/pmc_FETCH_SIZE" "$O/pmc_WRITE_SIZE" "$O/pmc_run.json" "${PMC_WORKLOAD:-10000000 Imp3D push-sum}" "${PMC_KERNEL:-k_ps_quiet<1>}" ;;
   cli)
     IFS=';' read -ra CASES <<< "${CLI_CASES:-10000000 Imp3D push-sum}"
     for c in "${CASES[@]}"; do

@@ -1,7 +1,7 @@
+# Round-3 A/B session (one gpurun call): GPU tests on the default build, then CLI convergence
+# times of the variant libraries and a whole-run kernel trace of the default build.
 set -o pipefail
-R="$GRAFT_REPO_ROOT"; cd "$R"; mkdir -p gpurun_out/mb
-timeout -k 10 60 rocprofv3 -L > gpurun_out/mb/counters.txt 2>&1; echo "list rc=$?"
-timeout -k 10 60 ./tools/microbench/persist > gpurun_out/mb/persist.txt 2>&1 && cat gpurun_out/mb/persist.txt &&
-timeout -k 10 60 ./tools/microbench/gatherpol > gpurun_out/mb/gatherpol.txt 2>&1 && cat gpurun_out/mb/gatherpol.txt &&
-OUT=cli VARIANTS="base g6 s96 s96g7 s80w8 s96w7" CLI_CASES="10000000 Imp3D push-sum;100000000 Imp3D push-sum" bash tools/gpu.sh cli &&
-OUT=ab ROUNDS=300 VARIANTS="base g6 s96 s96g7 s80w8 s96w7" KT_LINES=1 bash tools/gpu.sh ab
+R="$GRAFT_REPO_ROOT"; cd "$R"
+TEST_TIMEOUT=900 bash tools/gpu.sh tests &&
+OUT=cli VARIANTS="${VARIANTS:-old q7 q6 seg64 seg8 seg32}" CLI_CASES="${CLI_CASES:-10000000 Imp3D push-sum;100000000 Imp3D push-sum;2000000 Imp3D push-sum}" bash tools/gpu.sh cli &&
+OUT=c3 BENCH_ARGS="--no-cpu-baseline --steps 3" bash tools/gpu.sh bench
