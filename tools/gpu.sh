@@ -11,6 +11,7 @@
 #   cli     CLI convergence times of the variant libraries of $VARIANTS on each workload of
 #           $CLI_CASES ("N topo algo;N topo algo"), $REPS (default 3) interleaved runs
 #   loopab  `loop` for each variant library of $VARIANTS
+#   ktrun   kernel trace of one prof_run.py run ($ROUNDS, default: to convergence)
 #   pmcrun  FETCH_SIZE and WRITE_SIZE passes over a whole run (prof_run.py, $ROUNDS default: to
 #           convergence) -> tools/pmc_run_summary.py ($PMC_WORKLOAD, $PMC_KERNEL) into $O
 # Extra prof_run.py arguments: $PROF_ARGS; rounds: $ROUNDS; bench.py arguments: $BENCH_ARGS;
@@ -77,6 +78,8 @@ case $MODE in
         done
       done
     done ;;
+  ktrun)  # kernel trace of one prof_run.py run ($ROUNDS rounds, default: to convergence)
+    kt kt python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-1000000} ${PROF_ARGS} ;;
   loopab)
     for v in ${VARIANTS}; do
       GP_LIB=lib_$v kt "kt_$v" python3 "$R/tools/shard_loopback_prof.py" ${LOOP_ARGS} || exit $?
