@@ -178,13 +178,15 @@ struct Launch {
 int grid_for(uint32_t n);
 uint32_t span_for(uint32_t n, int grid);
 
-// Quiet-wave marks: one byte per segment of kActSeg actors (GP_ACT_SEG: 16, or 64 = one wave).
+// Quiet-wave marks: one byte per segment of kActSeg actors (GP_ACT_SEG: 4, 8, 16, 32, or 64 = one
+// wave).  4: C3 -8%, 100M -4% against 16 (profiles/round3/tail_ab); one mark per actor with
+// 1024-actor compaction was slower than 4 (scattered actors cost their own lines).
 #ifndef GP_ACT_SEG
-#define GP_ACT_SEG 16
+#define GP_ACT_SEG 4
 #endif
 constexpr uint32_t kActSeg = GP_ACT_SEG;
-constexpr uint32_t kActShift = kActSeg == 64u ? 6u : kActSeg == 32u ? 5u : kActSeg == 16u ? 4u : 3u;
-static_assert((1u << kActShift) == kActSeg, "GP_ACT_SEG: 8, 16, 32 or 64");
+constexpr uint32_t kActShift = kActSeg == 64u ? 6u : kActSeg == 32u ? 5u : kActSeg == 16u ? 4u : kActSeg == 8u ? 3u : 2u;
+static_assert((1u << kActShift) == kActSeg, "GP_ACT_SEG: 4, 8, 16, 32 or 64");
 
 // round kernels
 void launch_ps_pull(const RoundArgs& a, const Launch& l);

@@ -463,7 +463,8 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
 // actors and receive nothing, so that is their whole round — and then walks the marked
 // segments only, 64 / kActSeg of them per pass of its 64 lanes (each segment's actors stay
 // contiguous in a lane group, so the loads keep their coalescing).  With 64-actor marks nearly
-// every wave of the tail had work (86% at 3% active actors); 16-actor segments skip ~60%.
+// every wave of the tail had work (86% at 3% active actors); 4-actor segments (16 per pass) walk
+// about 3.8 actors per active one at 3% active actors (16-actor segments: 12.9).
 // One walk loop with one ps_actor call serves both the dense rounds and the tail (two inlined
 // copies of the actor body cost 4 spilled VGPRs and a wave per SIMD).
 // Walk state of the compacted tail (per wave): the next 64-segment chunk of the XCD group's span,
@@ -502,11 +503,13 @@ __device__ __forceinline__ bool tail_next(const RoundArgs& a, TailWalk& t, uint8
         const bool act = valid && a.act_prev[seg] == tag;
         if (valid && !act) {  // kActSeg direction bytes (the array is padded past the last actor)
             uint8_t* d = a.dir_cur + (size_t)seg * S;
+            static_assert(kDirNone == 7, "kDirNone bytes");
             if constexpr (S == 16u) {
                 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-                static_assert(kDirNone == 7, "kDirNone bytes");
                 const u4 none = {0x07070707u, 0x07070707u, 0x07070707u, 0x07070707u};
                 __builtin_nontemporal_store(none, reinterpret_cast<u4*>(d));
+            } else if constexpr (S == 4u) {
+                __builtin_nontemporal_store(0x07070707u, reinterpret_cast<uint32_t*>(d));
             } else {
 #pragma unroll
                 for (uint32_t i = 0; i < S; ++i) __builtin_nontemporal_store(kDirNone, d + i);
