@@ -190,7 +190,9 @@ constexpr uint32_t kLinkUnroll = GP_LINK_UNROLL;
 // instruction mix stays: bit 6 held row, 7 the six neighbours' direction bytes, 8 flags, 9 CSR
 // offsets (li = v, nl = 1 instead), 10 CSR sources, 11 link marks, 12 lpos, 13 fired-link
 // message gathers, 14 grid-hit message gathers, 15 only the +-G^2 grid-hit gathers, 16 only the
-// +-G^2 direction bytes.
+// +-G^2 direction bytes, 17 a link slot counts as fired iff its source id is 0 mod 7 (the
+// fired-link gathers keep their count without reading the marks), 18 the sender's link mark
+// stored into the cache-resident prefix.
 #ifndef GP_ABLATE
 #define GP_ABLATE 0
 #endif
@@ -246,6 +248,37 @@ constexpr bool kPreGrid = GP_PRE_GRID != 0;
 #define GP_WAVE_ADD 1
 #endif
 constexpr bool kWaveAdd = GP_WAVE_ADD != 0;
+
+// Cache policy of the link-mark stores (one random byte per fired link; GP_MARK_POL, A/B knob: 0
+// plain, 1 non-temporal, 2 non-temporal up to kMarkNtNodes nodes) in the one-GPU round kernel.  The marks of a round are
+// ~1.4M random bytes at 10M nodes that the next round reads back in CSR order; stored plainly they
+// cost 27 us of a 206 us all-sending round (a timing-only build storing them into a cache-resident
+// prefix ran 179 us, profiles/round3/mark_ab), stored non-temporally 6 us less (C3 -2%), while at
+// 100M nodes non-temporal marks were 1.8% slower over a run; sc1 / sc0 sc1 write-through stores
+// gained nothing.  The shard passes store their marks plainly (the unpack's non-temporal marks
+// cost 0.29 ms more per rank-round at C5 / 8, profiles/round3/mark_ab/loop_policies.txt).  GP_ACT_POL: the same choice for the quiet-segment marks (plain: nt was slower).
+#ifndef GP_MARK_POL
+#define GP_MARK_POL 2
+#endif
+#ifndef GP_ACT_POL
+#define GP_ACT_POL 0
+#endif
+constexpr uint32_t kMarkNtNodes = 1u << 25;
+template <int POL>
+__device__ __forceinline__ void byte_store(uint8_t* p, uint8_t x) {
+    if constexpr (POL == 1) {
+        __builtin_nontemporal_store(x, p);
+    } else {
+        *p = x;
+    }
+}
+__device__ __forceinline__ void mark_store(const RoundArgs& a, uint8_t* p, uint8_t x) {
+    if (GP_MARK_POL == 1 || (GP_MARK_POL == 2 && a.nodes <= kMarkNtNodes)) {  // uniform
+        byte_store<1>(p, x);
+    } else {
+        byte_store<0>(p, x);
+    }
+}
 
 // One 16-byte non-temporal store of a message (the round's messages cannot stay in L2 until the
 // next round reads them; streaming them leaves L2 to the rows that are re-read now).
@@ -400,7 +433,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
             // ---- level 3: the messages of the sources whose slot is marked
 #pragma unroll
             for (uint32_t k = 0; k < kLinkUnroll; ++k) {
-                lk[k] = k < nl && lc[k] == a.tag_prev;  // round-tagged marks: nothing to clear
+                lk[k] = k < nl && ((kAblate & 131072u) ? ls[k] % 7u == 0u : lc[k] == a.tag_prev);  // round tags
                 if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
                     lm[k] = a.rmsg_prev[li + k];
                 } else {
@@ -438,14 +471,16 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
     }
     __builtin_nontemporal_store(o.send ? (uint8_t)code : kDirNone, &a.dir_cur[v]);
     if constexpr (LM == 1 && kFuseLinkMarks) {  // the link pass's mark, written by the sender
-        if (o.send && code == kDirLink) a.lcnt_cur[a.lpos[ab<4096u>(v)]] = (uint8_t)a.tag_cur;
+        if (o.send && code == kDirLink) mark_store(a, &a.lcnt_cur[ab<262144u>(a.lpos[ab<4096u>(v)])], (uint8_t)a.tag_cur);
     }
     if (f != f0) a.flags[v] = f;
     if (o.conv_now) a.frozen[v] = o.msg;
     if (mark) {  // the waves with work in round r + 1: v's own if it still updates, its target's
         const uint8_t t = (uint8_t)link_tag(r + 1u);
-        if (!(f & 16u)) a.act_cur[v >> kActShift] = t;
-        if (o.send) a.act_cur[dir_target(g, v, code, code == kDirLink ? link_of(a.seed, v, a.nodes) : 0u) >> kActShift] = t;
+        if (!(f & 16u)) byte_store<GP_ACT_POL>(&a.act_cur[v >> kActShift], t);
+        if (o.send)
+            byte_store<GP_ACT_POL>(
+                &a.act_cur[dir_target(g, v, code, code == kDirLink ? link_of(a.seed, v, a.nodes) : 0u) >> kActShift], t);
     }
     return o.conv_now ? 1u : 0u;
 }
@@ -468,14 +503,23 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
 // One walk loop with one ps_actor call serves both the dense rounds and the tail (two inlined
 // copies of the actor body cost 4 spilled VGPRs and a wave per SIMD).
 // Walk state of the compacted tail (per wave): the next 64-segment chunk of the XCD group's span,
-// the marked segments of the current chunk (in LDS) and how many of them are walked.
+// the marks of that chunk and the one after it (prefetched: a chunk is opened without waiting for
+// its load), and the marked segments listed but not walked yet (in LDS).
+constexpr uint32_t kTailList = 128;  // >= 64 / kActSeg - 1 leftovers + one chunk of 64
+static_assert(kTailList >= 64u / kActSeg - 1u + 64u, "tail list capacity");
 struct TailWalk {
     uint32_t base, s1, stride, c, k;
     uint32_t* list;
+    uint32_t pf0, pf1;
 };
 
-__device__ __forceinline__ TailWalk tail_walk(const RoundArgs& a) {
-    __shared__ uint32_t seg_list[kBlock];
+__device__ __forceinline__ uint32_t tail_mark(const RoundArgs& a, const TailWalk& t, uint32_t chunk) {
+    const uint32_t seg = chunk + (threadIdx.x & 63u);
+    return chunk < t.s1 && seg < t.s1 ? a.act_prev[seg] : 0u;
+}
+
+__device__ __forceinline__ TailWalk tail_walk(const RoundArgs& a, bool tail) {
+    __shared__ uint32_t seg_list[kBlock / 64u * kTailList];
     TailWalk t;
     const uint32_t nseg = (a.hi + kActSeg - 1u) >> kActShift;  // one GPU: actors [0, hi)
     const uint32_t grp = blockIdx.x & 7u, wpg = (gridDim.x >> 3) * (kBlock / 64u);
@@ -486,21 +530,33 @@ __device__ __forceinline__ TailWalk tail_walk(const RoundArgs& a) {
     t.base = s0 + wid * 64u;
     t.stride = wpg * 64u;
     t.c = t.k = 0;
-    t.list = seg_list + (threadIdx.x & ~63u);
+    t.list = seg_list + (threadIdx.x >> 6) * kTailList;
+    t.pf0 = tail ? tail_mark(a, t, t.base) : 0u;
+    t.pf1 = tail ? tail_mark(a, t, t.base + t.stride) : 0u;
     return t;
 }
 
 // The next actor of this lane in the compacted tail walk (a.hi: none this pass); false when the
-// wave's span is done.  Wave-uniform.  A chunk's unmarked segments get "send nothing"
-// (kDirNone) direction bytes as the chunk is opened.
+// wave's span is done.  Wave-uniform.  Chunks are opened until a full pass of 64 / kActSeg marked
+// segments is listed (or the span ends), so a pass of the late tail, where a chunk holds one or
+// two marked segments, keeps its 64 lanes busy (one pass per chunk left 1-2 segments per pass);
+// each chunk's unmarked segments get "send nothing" (kDirNone) direction bytes as it is opened.
 __device__ __forceinline__ bool tail_next(const RoundArgs& a, TailWalk& t, uint8_t tag, uint32_t& v) {
     constexpr uint32_t S = kActSeg, PER = 64u / kActSeg;
     const uint32_t lane = threadIdx.x & 63u;
-    while (t.k >= t.c) {
-        if (t.base >= t.s1) return false;
+    while (t.c - t.k < PER && t.base < t.s1) {
+        if (t.k) {  // fewer than PER left: move them to the front (one read, then one write)
+            const uint32_t left = t.c - t.k;
+            const uint32_t x = lane < left ? t.list[t.k + lane] : 0u;
+            if (lane < left) t.list[lane] = x;
+            t.c = left;
+            t.k = 0;
+        }
         const uint32_t seg = t.base + lane;
         const bool valid = seg < t.s1;
-        const bool act = valid && a.act_prev[seg] == tag;
+        const bool act = valid && t.pf0 == tag;
+        t.pf0 = t.pf1;
+        t.pf1 = tail_mark(a, t, t.base + 2u * t.stride);
         if (valid && !act) {  // kActSeg direction bytes (the array is padded past the last actor)
             uint8_t* d = a.dir_cur + (size_t)seg * S;
             static_assert(kDirNone == 7, "kDirNone bytes");
@@ -516,11 +572,11 @@ __device__ __forceinline__ bool tail_next(const RoundArgs& a, TailWalk& t, uint8
             }
         }
         const uint64_t m = __ballot(act);
-        if (act) t.list[mbcnt64(m)] = seg;
-        t.c = (uint32_t)__popcll(m);
-        t.k = 0;
+        if (act) t.list[t.c + mbcnt64(m)] = seg;
+        t.c += (uint32_t)__popcll(m);
         t.base += t.stride;
     }
+    if (t.k >= t.c) return false;
     const uint32_t j = t.k + lane / S;
     v = j < t.c ? t.list[j] * S + lane % S : a.hi;
     t.k += PER;
@@ -573,8 +629,8 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a) {
     const bool skip = Q && r >= 2u && a.total[r - 2] >= a.act_thr;  // F(r - 1) marked round r
     const uint8_t tag = (uint8_t)a.tag_cur;  // link_tag(r)
     if constexpr (Q && kActSeg < 64u) {
-        TailWalk t = tail_walk(a);
         const bool tail = skip;  // block-uniform: the compacted segment walk of the run's tail
+        TailWalk t = tail_walk(a, tail);
         for (;;) {
             uint32_t u;
             if (tail) {
@@ -1049,7 +1105,8 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
             else if (gossip) a.lcnt_cur[t] = (uint8_t)((e >> 31) + 1u);
             else {  // the sender's message into the receiver's slot, the slot marked
                 a.rmsg_cur[t] = in.msg[i];
-                a.lcnt_cur[t] = (uint8_t)a.tag_cur;
+                a.lcnt_cur[t] = (uint8_t)a.tag_cur;  // plain: non-temporal marks and messages
+                                                     // cost 0.29 ms more per round (C5 / 8)
             }
         }
     }
