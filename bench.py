@@ -171,13 +171,18 @@ def gpu_same_window(eng, rounds, reps=3):
 
 
 def roofline(ks, bytes_per_update, actors, wl):
-    """Round roofline: SURVEY §8(d) bytes per node-update x this rank's actors over the
-    measured duration of one round = the round kernel + the pass that completes it (link
-    scatter), both timed with hipEvents on the engine's stream inside the timed steps."""
+    """Round roofline: SURVEY §8(d) bytes per node-update x the node-updates one launch performs
+    over the measured duration of one round = the round kernel + the pass that completes it (link
+    scatter), both timed with hipEvents on the engine's stream inside the timed steps.  The
+    node-updates per launch are the engine's own count (gp_kstats.work_per_launch): every actor of
+    the range, except that the one-GPU quiet-tail kernel counts the actors it walks, so the
+    converged tail, where a round touches a few percent of the actors, is not credited 112 B for
+    every actor (that figure, `frac_all_actors`, exceeds 1 once the tail is cheap)."""
     if not ks["launches"]:
         return None
     round_ms = ks["avg_ms"] + ks["aux_avg_ms"]
-    algo_bytes = bytes_per_update * actors
+    units = ks.get("work_per_launch") or float(actors)
+    algo_bytes = bytes_per_update * units
     achieved = algo_bytes / (round_ms * 1e-3) / 1e9
     kernels = [ks["kernel"]] + ([ks["aux_kernel"]] if ks["aux_kernel"] else [])
     traffic, traffic_rounds = pmc_traffic(kernels, wl)
@@ -188,7 +193,9 @@ def roofline(ks, bytes_per_update, actors, wl):
             "hbm_measured_frac": round(measured, 4) if measured else None,
             "kernel": " + ".join(kernels), "avg_kernel_ms": round(ks["avg_ms"], 5),
             "avg_aux_ms": round(ks["aux_avg_ms"], 5), "round_ms": round(round_ms, 5),
-            "bytes_per_launch": algo_bytes, "bytes_per_update": bytes_per_update, "launches": ks["launches"],
+            "bytes_per_launch": algo_bytes, "bytes_per_update": bytes_per_update,
+            "updates_per_launch": round(units, 1), "actors": actors, "launches": ks["launches"],
+            "frac_all_actors": round(bytes_per_update * actors / (round_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "layout_bytes_per_launch": ks["bytes_per_launch"],
             "layout_frac": round(ks["bytes_per_launch"] / (ks["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 

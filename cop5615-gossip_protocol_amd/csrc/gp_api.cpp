@@ -163,6 +163,8 @@ struct Handle {
     hipEvent_t ev_a = nullptr, ev_b = nullptr;
     int64_t k_launches = 0;
     double k_total_ms = 0.0, k_aux_ms = 0.0;
+    unsigned long long* work = nullptr;  // actors walked by the quiet kernel (kernel statistics)
+    int64_t work_rounds = 0;             // real rounds run while it counted
     std::vector<long long> timed_round;  // sharded: round applied by each timed kernel
     int64_t timed_count = 0;
 
@@ -238,6 +240,7 @@ struct Handle {
         a.rmsg_cur = rmsg[c];
         a.dir_prev = dir[p];
         a.dir_cur = dir[c];
+        a.work = (cfg.flags & GP_FLAG_KERNEL_TIMING) && act[0] ? work : nullptr;
         a.flags = flags;
         a.frozen = frozen;
         if (gossip) {
@@ -689,6 +692,7 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         } else if (timing && (rc = accumulate_timing(h, (real + kTimeEvery - 1) / kTimeEvery))) {
             return rc;
         }
+        if (timing) h->work_rounds += real;
         // Batches double up to 256 rounds; once 31/32 of the nodes have reported, the run is in
         // its tail and the batch shrinks to GP_TAIL_BATCH, so fewer rounds are launched past
         // convergence (each exits at its gate, but still costs a launch).  A tail batch that
@@ -1093,6 +1097,9 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
             (h->g.actors >= kQuietMinActors || (cfg->flags & GP_FLAG_QUIET_WAVES))) {  // quiet-wave marks
             for (int i = 0; i < 2; ++i)
                 if ((rc = h->alloc(&h->act[i], act_bytes(h)))) return bail(rc);
+            if ((rc = h->alloc(&h->work, 1))) return bail(rc);
+            if (hipMemsetAsync(h->work, 0, sizeof *h->work, h->stream) != hipSuccess)
+                return bail(fail(GP_EHIP, "hipMemsetAsync failed"));
             h->act_thr = (uint32_t)((uint64_t)h->lay.nodes * GP_ACT_PCT / 100u);
         }
         if (h->generic) {  // single-GPU only: whole graph
@@ -1650,10 +1657,19 @@ int gp_kernel_stats(void* handle, gp_kstats* out, int32_t reset_counters) {
     std::snprintf(out->kernel, sizeof out->kernel, "%s", round_kernel_name(h));
     out->aux_avg_ms = h->k_launches ? h->k_aux_ms / (double)h->k_launches : 0.0;
     std::snprintf(out->aux_kernel, sizeof out->aux_kernel, "%s", aux_kernel_name(h));
+    out->work_per_launch = (double)h->own();
+    if (h->act[0] && h->work) {  // the quiet kernel counts the actors it walks
+        unsigned long long w = 0;
+        HIP_TRY(hipMemcpyAsync(&w, h->work, sizeof w, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        out->work_per_launch = h->work_rounds ? (double)w / (double)h->work_rounds : 0.0;
+    }
     if (reset_counters) {
         h->k_launches = 0;
         h->k_total_ms = 0.0;
         h->k_aux_ms = 0.0;
+        h->work_rounds = 0;
+        if (h->work) HIP_TRY(hipMemsetAsync(h->work, 0, sizeof *h->work, h->stream));
     }
     return GP_OK;
 }

@@ -111,6 +111,9 @@ struct RoundArgs {
     uint32_t* bcnt_cur;
     uint32_t* tgt_cur;        // destination of v's message (UINT32_MAX none)
     uint32_t* pos_cur;        // slot of v's message inside its destination bucket
+    // kernel statistics (GP_FLAG_KERNEL_TIMING, one-GPU quiet kernel): actors walked, summed over
+    // launches; null: not counted
+    unsigned long long* work;
 };
 
 // Shard exchange (gp_shard_*).  Send chunk to peer q (built by this rank) and receive chunk from

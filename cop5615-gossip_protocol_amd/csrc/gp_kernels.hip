@@ -63,6 +63,20 @@ __device__ __forceinline__ void block_add(uint32_t c, uint32_t* parts, long long
     }
 }
 
+// Block-wide sum of one u32 per thread added to a u64 counter (kernel statistics only).
+__device__ __forceinline__ void block_add_u64(uint32_t c, unsigned long long* ctr) {
+    __shared__ uint32_t red[kBlock / 64];
+    c = wave_sum(c);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+#pragma unroll
+        for (int i = 0; i < kBlock / 64; ++i) t += red[i];
+        if (t) atomicAdd(ctr, t);
+    }
+}
+
 // The same count added per wave (small graphs: no LDS round trip and no block barrier at the end
 // of the round; most waves have nothing to add).
 __device__ __forceinline__ void wave_add(uint32_t c, uint32_t* parts, long long a) {
@@ -631,6 +645,7 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a) {
     if constexpr (Q && kActSeg < 64u) {
         const bool tail = skip;  // block-uniform: the compacted segment walk of the run's tail
         TailWalk t = tail_walk(a, tail);
+        uint32_t walked = 0;
         for (;;) {
             uint32_t u;
             if (tail) {
@@ -640,9 +655,13 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a) {
                 u = v;
                 v += step;
             }
-            if (u < a.hi) newly += ps_actor<LM>(a, g, r, u, mark);
+            if (u < a.hi) {
+                newly += ps_actor<LM>(a, g, r, u, mark);
+                ++walked;
+            }
         }
         block_add(newly, a.parts, r);
+        if (a.work) block_add_u64(walked, a.work);
         return;
     }
     for (; v < end; v += step) {

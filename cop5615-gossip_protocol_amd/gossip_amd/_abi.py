@@ -13,7 +13,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, os.environ.get("GP_LIB", "lib"), "libgossip_hip.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "gossip_hip.h")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 TOPOLOGIES = {"line": 0, "full": 1, "2D": 2, "Imp3D": 3, "3D": 4}
 ALGOS = {"gossip": 0, "push-sum": 1}
 FLAG_KERNEL_TIMING = 1
@@ -47,7 +47,7 @@ class Status(C.Structure):
 class KStats(C.Structure):
     _fields_ = [("launches", C.c_int64), ("total_ms", C.c_double), ("avg_ms", C.c_double),
                 ("bytes_per_launch", C.c_double), ("kernel", C.c_char * 64),
-                ("aux_avg_ms", C.c_double), ("aux_kernel", C.c_char * 64)]
+                ("aux_avg_ms", C.c_double), ("aux_kernel", C.c_char * 64), ("work_per_launch", C.c_double)]
 
 
 class ShardLayout(C.Structure):

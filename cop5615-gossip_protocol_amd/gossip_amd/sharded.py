@@ -135,7 +135,8 @@ class HipShard:
         _abi.check(self.lib.gp_kernel_stats(self.h, C.byref(ks), 1 if reset else 0))
         return {"launches": ks.launches, "total_ms": ks.total_ms, "avg_ms": ks.avg_ms,
                 "bytes_per_launch": ks.bytes_per_launch, "kernel": ks.kernel.decode(),
-                "aux_avg_ms": ks.aux_avg_ms, "aux_kernel": ks.aux_kernel.decode()}
+                "aux_avg_ms": ks.aux_avg_ms, "aux_kernel": ks.aux_kernel.decode(),
+                "work_per_launch": ks.work_per_launch}
 
     def close(self):
         if getattr(self, "h", None):

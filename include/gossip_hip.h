@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 3
+#define GP_ABI_VERSION 4
 
 /* program.fs:151 "line", :191 "full", :227 "2D", :267 "Imp3D"; "3D" is build-defined (Q9) */
 enum gp_topology { GP_LINE = 0, GP_FULL = 1, GP_TWO_D = 2, GP_IMP3D = 3, GP_THREE_D = 4 };
@@ -101,6 +101,9 @@ typedef struct gp_kstats {
     char kernel[64];    /* name of the dominant round kernel                               */
     double aux_avg_ms;  /* the pass that completes a round after it (0 if none)            */
     char aux_kernel[64];
+    double work_per_launch; /* actor updates one launch of it performs, mean over the rounds run
+                               since the last reset: every actor of the range, except that the
+                               one-GPU quiet-tail kernel counts the actors it walks (ABI 4)      */
 } gp_kstats;
 
 int gp_abi_version(void);

@@ -248,3 +248,36 @@ def test_quiet_waves_default_and_reset():
         gpu.reset()
     gpu.close()
     cpu.close()
+
+
+def test_quiet_work_count_vs_oracle():
+    """gp_kstats.work_per_launch of the quiet kernel (bench.py's roofline units) is the exact count
+    of the actors it walks: every actor in a round without marks, else every actor of each 4-actor
+    segment that holds an unconverged actor or a target of the previous round's messages (the
+    marks of DESIGN.md §4), recomputed here from the oracle's per-round state."""
+    n, seed, seg, pct = 20000, 7, 4, 99
+    gpu = Simulator(n, "Imp3D", "push-sum", seed=seed, quiet_waves=True, kernel_timing=True)
+    cpu = oracle.OracleSim(n, "Imp3D", "push-sum", seed=seed)
+    gs = gpu.step(1 << 20)
+    ks = gpu.kernel_stats()
+    actors, thr = gpu.actors, gpu.nodes * pct // 100
+    trace = gpu.read_trace()
+    walked = actors  # F(0)
+    cpu.step(1, threads=8)
+    for r in range(1, gs.round):
+        dst, _, _ = cpu.read_messages()  # sent in round r - 1
+        _, _, fl = cpu.read_pushsum()    # after round r - 1
+        if r >= 2 and trace[r - 2] >= thr:
+            act = (fl & 16) == 0
+            act[gpu.nodes:] = False  # the isolated actor has no neighbours and never updates
+            act[dst[dst < actors].astype(np.int64)] = True
+            marked = np.zeros((actors + seg - 1) // seg, bool)
+            marked[np.nonzero(act)[0] // seg] = True
+            walked += int(np.minimum(seg, actors - seg * np.nonzero(marked)[0]).sum())
+        else:
+            walked += actors
+        cpu.step(1, threads=8)
+    assert ks["work_per_launch"] * gs.round == pytest.approx(walked, rel=0, abs=0.5)
+    assert ks["work_per_launch"] < actors
+    gpu.close()
+    cpu.close()
