@@ -12,6 +12,7 @@
 #           $CLI_CASES ("N topo algo;N topo algo"), $REPS (default 3) interleaved runs
 #   loopab  `loop` for each variant library of $VARIANTS
 #   ktrun   kernel trace of one prof_run.py run ($ROUNDS, default: to convergence)
+#   ktrun_bench  kernel trace of bench.py with the arguments given as the second argument
 #   pmcrun  FETCH_SIZE and WRITE_SIZE passes over a whole run (prof_run.py, $ROUNDS default: to
 #           convergence) -> tools/pmc_run_summary.py ($PMC_WORKLOAD, $PMC_KERNEL) into $O
 # Extra prof_run.py arguments: $PROF_ARGS; rounds: $ROUNDS; bench.py arguments: $BENCH_ARGS;
@@ -78,6 +79,8 @@ case $MODE in
         done
       done
     done ;;
+  ktrun_bench)  # kernel trace of bench.py with the arguments in $2
+    kt kt python3 "$R/bench.py" $2 ;;
   ktrun)  # kernel trace of one prof_run.py run ($ROUNDS rounds, default: to convergence)
     kt kt python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-1000000} ${PROF_ARGS} ;;
   loopab)

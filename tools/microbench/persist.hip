@@ -88,13 +88,63 @@ __global__ __launch_bounds__(kBlock) void k_persist_xcd(int* a, int* b, int roun
     }
 }
 
+// (c) one XCD only: the blocks running on XCD 0 (hardware XCC_ID, not blockIdx) do all the work and
+// synchronise through that XCD's L2, which they share: release = s_waitcnt vmcnt(0) (the vector L1
+// writes through), the arrival atomic at workgroup scope (performed in the shared L2), acquire =
+// invalidate the vector L1 (buffer_inv sc0).  The other blocks exit at once.  Membership: every
+// block registers, then all wait until every block of the grid has started (one device-wide
+// rendezvous), so the XCD-0 member count is final before round 0.
+__device__ __forceinline__ unsigned xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u; }
+
+__global__ __launch_bounds__(kBlock) void k_persist_one_xcd(int* a, int* b, int rounds, unsigned* started,
+                                                            unsigned* members, unsigned* arrive, unsigned* cnt,
+                                                            unsigned* err) {
+    __shared__ unsigned rank_s, nmem_s;
+    const bool mine = xcc_id() == 0u;
+    if (threadIdx.x == 0) {
+        rank_s = mine ? atomicAdd(members, 1u) : 0u;
+        atomicAdd(started, 1u);
+        if (!spin_until(started, gridDim.x)) atomicOr(err, 1u);
+        nmem_s = ld_relaxed(members);
+    }
+    __syncthreads();
+    if (!mine || ld_relaxed(err)) return;
+    const unsigned rank = rank_s, nmem = nmem_s;
+    for (int r = 0; r < rounds; ++r) {
+        const int* in = (r & 1) ? b : a;
+        int* out = (r & 1) ? a : b;
+        for (int i = (int)(rank * kBlock + threadIdx.x); i < kN; i += (int)(nmem * kBlock)) {
+            const int j = (int)(((long long)i * 7919 + r) % kN);
+            out[i] = in[j] + 1;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __hip_atomic_fetch_add(cnt + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            long long spins = 0;
+            while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(r + 1) * nmem) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kSpinCap) {
+                    atomicOr(err, 1u);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        asm volatile("buffer_inv sc0" ::: "memory");
+        if (ld_relaxed(err)) return;
+    }
+}
+
 int main() {
     const int R = 2000;
     const int grid = (kN + kBlock - 1) / kBlock;  // 391: every block resident (<= 8 per CU)
     int *a, *b;
-    unsigned *ctr, *sub, *top, *cnt, *err;
+    unsigned *ctr, *sub, *top, *cnt, *err, *started, *members, *arrive;
     if (hipMalloc(&a, kN * 4) || hipMalloc(&b, kN * 4) || hipMalloc(&ctr, 4) || hipMalloc(&sub, 8 * 32 * 4) ||
-        hipMalloc(&top, 4) || hipMalloc(&cnt, R * 4) || hipMalloc(&err, 4))
+        hipMalloc(&top, 4) || hipMalloc(&cnt, R * 4) || hipMalloc(&err, 4) || hipMalloc(&started, 4) ||
+        hipMalloc(&members, 4) || hipMalloc(&arrive, 4))
         return 1;
     (void)hipMemset(a, 0, kN * 4);
     (void)hipMemset(b, 0, kN * 4);
@@ -130,6 +180,38 @@ int main() {
                 printf("persistent, %s barrier + count (%d blocks): %.2f us/round%s\n", v ? "XCD-hierarchical" : "flat",
                        grid, ms * 1000.0 / R, e ? " (BARRIER TIMED OUT)" : "");
         }
+    }
+    // (c): 8 x 32 blocks, so about 32 land on XCD 0 (one per CU); the result is checked against
+    // the launch-per-round result of the same rounds
+    for (int pass = 0; pass < 2; ++pass) {
+        (void)hipMemsetAsync(a, 0, kN * 4, s);
+        (void)hipMemsetAsync(b, 0, kN * 4, s);
+        (void)hipMemsetAsync(started, 0, 4, s);
+        (void)hipMemsetAsync(members, 0, 4, s);
+        (void)hipMemsetAsync(arrive, 0, 4, s);
+        (void)hipMemsetAsync(cnt, 0, R * 4, s);
+        (void)hipMemsetAsync(err, 0, 4, s);
+        float ms = 0;
+        (void)hipEventRecord(e0, s);
+        hipLaunchKernelGGL(k_persist_one_xcd, dim3(256), dim3(kBlock), 0, s, a, b, R, started, members, arrive, cnt, err);
+        (void)hipEventRecord(e1, s);
+        (void)hipEventSynchronize(e1);
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        unsigned e = 0, m = 0;
+        (void)hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(&m, members, 4, hipMemcpyDeviceToHost);
+        static int got[kN], want[kN];
+        (void)hipMemcpy(got, (R & 1) ? b : a, kN * 4, hipMemcpyDeviceToHost);
+        (void)hipMemsetAsync(a, 0, kN * 4, s);
+        (void)hipMemsetAsync(b, 0, kN * 4, s);
+        for (int r = 0; r < R; ++r) hipLaunchKernelGGL(k_round, dim3(grid), dim3(kBlock), 0, s, (r & 1) ? b : a, (r & 1) ? a : b, r);
+        (void)hipMemcpy(want, (R & 1) ? b : a, kN * 4, hipMemcpyDeviceToHost);
+        int bad = 0;
+        for (int i = 0; i < kN; ++i) bad += got[i] != want[i];
+        if (pass)
+            printf("persistent on one XCD, L2-local barrier + count (%u blocks on XCD 0): %.2f us/round, %d of %d "
+                   "elements differ from the launch-per-round result%s\n",
+                   m, ms * 1000.0 / R, bad, kN, e ? " (BARRIER TIMED OUT)" : "");
     }
     printf("status %s\n", hipGetErrorString(hipGetLastError()));
     return 0;
