@@ -189,6 +189,15 @@ __device__ __forceinline__ T load_sel(const T* base, bool pred, uint32_t idx, ui
     return base[pred ? idx : fallback];
 }
 
+// The message loads of lanes without a grid hit / fired link read one row shared by the whole
+// grid (msg_prev[lo], 1) rather than the actor's own row (0, A/B knob): a wave's predicated-off
+// lanes then touch one line instead of eight, and a converged actor, which never reads its own
+// row, no longer pulls it in (all-sending C3 round 195.5 -> 189.8 us, profiles/round3/fallback_ab).
+#ifndef GP_MSG_FALLBACK_LO
+#define GP_MSG_FALLBACK_LO 1
+#endif
+constexpr bool kMsgFallbackLo = GP_MSG_FALLBACK_LO != 0;
+
 // Link slots scanned with unrolled loads before the (rare) tail loop.
 #ifndef GP_LINK_UNROLL
 #define GP_LINK_UNROLL 4
@@ -395,7 +404,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                         : load_sel(a.msg_prev, gs[j] != 0xFFFFFFFFu,
                                    (gs[j] == v - g.plane || gs[j] == v + g.plane) ? ab<32768u>(ab<16384u>(gs[j]))
                                                                                 : ab<16384u>(gs[j]),
-                                   v);
+                                   kMsgFallbackLo ? a.lo : v);
         uint32_t pend = hits;  // PRE: grid hits not yet added
         // A converged actor only relays what arrives (program.fs:125-127): its held (S,W) and so
         // its message row are not read (more than half of the C3 run's actor-rounds).  Issued
@@ -451,7 +460,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                 if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
                     lm[k] = a.rmsg_prev[li + k];
                 } else {
-                    lm[k] = load_sel(a.msg_prev, lk[k], ab<8192u>(ls[k]), v);
+                    lm[k] = load_sel(a.msg_prev, lk[k], ab<8192u>(ls[k]), kMsgFallbackLo ? a.lo : v);
                 }
             }
 #pragma unroll
