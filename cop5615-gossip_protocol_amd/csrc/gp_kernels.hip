@@ -183,7 +183,10 @@ __device__ __forceinline__ uint32_t slot_bit(uint32_t k) { return k == 0 ? 16u :
 __device__ __forceinline__ uint32_t slot_code(uint32_t k) { return k == 0 ? 5u : k == 1 ? 3u : k == 2 ? 1u : k == 3 ? 0u : k == 4 ? 2u : 4u; }
 
 // Branch-free load: a predicated-off lane reads `fallback` (an element it already touches),
-// so hipcc emits straight-line loads instead of one basic block + vmcnt(0) per condition.
+// so hipcc emits straight-line loads instead of one basic block + vmcnt(0) per condition
+// (round 3, C3 all-sending rounds: the grid-hit and link message loads exec-masked 298 vs 202
+// us; a wave-uniform skip of the 3rd / 4th link message load when no lane needs it 244 vs 200
+// us, profiles/round3/load_shape_ab).
 template <class T>
 __device__ __forceinline__ T load_sel(const T* base, bool pred, uint32_t idx, uint32_t fallback) {
     return base[pred ? idx : fallback];
@@ -215,7 +218,8 @@ constexpr uint32_t kLinkUnroll = GP_LINK_UNROLL;
 // message gathers, 14 grid-hit message gathers, 15 only the +-G^2 grid-hit gathers, 16 only the
 // +-G^2 direction bytes, 17 a link slot counts as fired iff its source id is 0 mod 7 (the
 // fired-link gathers keep their count without reading the marks), 18 the sender's link mark
-// stored into the cache-resident prefix.
+// stored into the cache-resident prefix, 19 no loads of the 3rd / 4th link message (the 16-byte
+// load instructions themselves), 20 no load of the 3rd grid-hit message.
 #ifndef GP_ABLATE
 #define GP_ABLATE 0
 #endif
@@ -400,7 +404,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
         double2 gm[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-            gm[j] = PRE ? make_double2(0.0, 0.0)
+            gm[j] = (PRE || ((kAblate & 1048576u) && j == 2)) ? make_double2(0.0, 0.0)
                         : load_sel(a.msg_prev, gs[j] != 0xFFFFFFFFu,
                                    (gs[j] == v - g.plane || gs[j] == v + g.plane) ? ab<32768u>(ab<16384u>(gs[j]))
                                                                                 : ab<16384u>(gs[j]),
@@ -460,7 +464,9 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                 if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
                     lm[k] = a.rmsg_prev[li + k];
                 } else {
-                    lm[k] = load_sel(a.msg_prev, lk[k], ab<8192u>(ls[k]), kMsgFallbackLo ? a.lo : v);
+                    lm[k] = ((kAblate & 524288u) && k >= 2u)
+                                ? make_double2(0.0, 0.0)
+                                : load_sel(a.msg_prev, lk[k], ab<8192u>(ls[k]), kMsgFallbackLo ? a.lo : v);
                 }
             }
 #pragma unroll
