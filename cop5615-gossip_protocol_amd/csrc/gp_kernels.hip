@@ -206,6 +206,14 @@ constexpr bool kMsgFallbackLo = GP_MSG_FALLBACK_LO != 0;
 #define GP_LINK_UNROLL 4
 #endif
 constexpr uint32_t kLinkUnroll = GP_LINK_UNROLL;
+// One GPU: message loads issued for the first GP_FIRED_LOADS fired link slots of an actor, the
+// others on demand (GP_LINK_UNROLL: one per unrolled slot, fired or not).  1: C3 -3%, 100M -1%
+// against 4 (each predicated 16-byte load instruction costs ~1.5% of an all-sending round,
+// profiles/round3/load_shape_ab); 2: C3 -2%, 100M +0.5%.
+#ifndef GP_FIRED_LOADS
+#define GP_FIRED_LOADS 1
+#endif
+constexpr uint32_t kFiredLoads = GP_FIRED_LOADS;
 
 // Timing-only builds (tools/variants) may drop parts of the round kernel to price them; the
 // product is built with 0, and the results of any other value are wrong by construction.
@@ -219,7 +227,7 @@ constexpr uint32_t kLinkUnroll = GP_LINK_UNROLL;
 // +-G^2 direction bytes, 17 a link slot counts as fired iff its source id is 0 mod 7 (the
 // fired-link gathers keep their count without reading the marks), 18 the sender's link mark
 // stored into the cache-resident prefix, 19 no loads of the 3rd / 4th link message (the 16-byte
-// load instructions themselves), 20 no load of the 3rd grid-hit message.
+// load instructions themselves), 20 no load of the 3rd grid-hit message, 21 no loads of the 3rd / 4th CSR source and mark.
 #ifndef GP_ABLATE
 #define GP_ABLATE 0
 #endif
@@ -451,30 +459,73 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
         if (LM) {
             uint32_t ls[kLinkUnroll];
 #pragma unroll
-            for (uint32_t k = 0; k < kLinkUnroll; ++k) ls[k] = load_sel(a.rev_src, k < nl, ab<1024u>(li + k), a.slot_lo);
+            for (uint32_t k = 0; k < kLinkUnroll; ++k)
+                ls[k] = ((kAblate & 2097152u) && k >= 2u) ? li + k : load_sel(a.rev_src, k < nl, ab<1024u>(li + k), a.slot_lo);
             bool lk[kLinkUnroll];
             double2 lm[kLinkUnroll];
             uint8_t lc[kLinkUnroll];
 #pragma unroll
-            for (uint32_t k = 0; k < kLinkUnroll; ++k) lc[k] = load_sel(a.lcnt_prev, k < nl, ab<2048u>(li + k), a.slot_lo);
+            for (uint32_t k = 0; k < kLinkUnroll; ++k)
+                lc[k] = ((kAblate & 2097152u) && k >= 2u) ? (uint8_t)(li >> 3) : load_sel(a.lcnt_prev, k < nl, ab<2048u>(li + k), a.slot_lo);
             // ---- level 3: the messages of the sources whose slot is marked
 #pragma unroll
-            for (uint32_t k = 0; k < kLinkUnroll; ++k) {
-                lk[k] = k < nl && ((kAblate & 131072u) ? ls[k] % 7u == 0u : lc[k] == a.tag_prev);  // round tags
-                if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
-                    lm[k] = a.rmsg_prev[li + k];
-                } else {
-                    lm[k] = ((kAblate & 524288u) && k >= 2u)
-                                ? make_double2(0.0, 0.0)
-                                : load_sel(a.msg_prev, lk[k], ab<8192u>(ls[k]), kMsgFallbackLo ? a.lo : v);
-                }
-            }
-#pragma unroll
             for (uint32_t k = 0; k < kLinkUnroll; ++k)
-                if (lk[k]) {
-                    flush(ls[k]);
-                    add(lm[k]);
+                lk[k] = k < nl && ((kAblate & 131072u) ? ls[k] % 7u == 0u : lc[k] == a.tag_prev);  // round tags
+            if constexpr (LM == 1 && kFiredLoads < kLinkUnroll) {
+                // one GPU: load the messages of the first kFiredLoads FIRED slots only (about one
+                // slot in seven fires: 0.14 messages per actor), the rest on demand (rare)
+                uint32_t rest = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < kLinkUnroll; ++k) rest |= lk[k] ? 1u << k : 0u;
+                uint32_t fs[kFiredLoads];
+                bool fv[kFiredLoads];
+                double2 fm[kFiredLoads];
+#pragma unroll
+                for (uint32_t j = 0; j < kFiredLoads; ++j) {
+                    const uint32_t k = (uint32_t)__builtin_ctz(rest | (1u << kLinkUnroll));
+                    fv[j] = rest != 0u;
+                    uint32_t u = ls[0];
+#pragma unroll
+                    for (uint32_t q = 1; q < kLinkUnroll; ++q) u = k == q ? ls[q] : u;
+                    fs[j] = u;
+                    rest &= rest - 1u;
                 }
+#pragma unroll
+                for (uint32_t j = 0; j < kFiredLoads; ++j)
+                    fm[j] = load_sel(a.msg_prev, fv[j], ab<8192u>(fs[j]), kMsgFallbackLo ? a.lo : v);
+#pragma unroll
+                for (uint32_t j = 0; j < kFiredLoads; ++j)
+                    if (fv[j]) {
+                        flush(fs[j]);
+                        add(fm[j]);
+                    }
+                while (rest) {  // rare: more than kFiredLoads of the unrolled slots fired
+                    const uint32_t k = (uint32_t)__builtin_ctz(rest);
+                    uint32_t u = ls[0];
+#pragma unroll
+                    for (uint32_t q = 1; q < kLinkUnroll; ++q) u = k == q ? ls[q] : u;
+                    flush(u);
+                    add(a.msg_prev[u]);
+                    rest &= rest - 1u;
+                }
+            } else {
+#pragma unroll
+                for (uint32_t k = 0; k < kLinkUnroll; ++k) {
+                    if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
+                        lm[k] = a.rmsg_prev[li + k];
+                    } else {
+                        lm[k] = ((kAblate & 524288u) && k >= 2u)
+                                    ? make_double2(0.0, 0.0)
+                                    : load_sel(a.msg_prev, lk[k], ab<8192u>(ls[k]), kMsgFallbackLo ? a.lo : v);
+                    }
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < kLinkUnroll; ++k)
+                    if (lk[k]) {
+                        flush(ls[k]);
+                        add(lm[k]);
+                    }
+            }
             for (uint32_t k = kLinkUnroll; k < nl; ++k) {  // rare: more than kLinkUnroll sources
                 if (a.lcnt_prev[li + k] == a.tag_prev) {
                     const uint32_t u = a.rev_src[li + k];
