@@ -232,6 +232,17 @@ constexpr uint32_t kFiredLoads = GP_FIRED_LOADS;
 #define GP_ABLATE 0
 #endif
 constexpr uint32_t kAblate = GP_ABLATE;
+// The CSR offsets of v (rev_off[v], rev_off[v + 1]) as one 8-byte load, the four unrolled
+// slots' sources as one 16-byte load and their marks as two dwords (1), or one load per element
+// (0, A/B knob).  Dword-aligned 8- and 16-byte loads (and byte-aligned ones) return the right
+// bytes on gfx950 (tools/microbench/unaligned.hip).  1: C3 -5.9%, 100M -6.1%
+// (profiles/round3/csr_vec_ab).  The marks as one byte-aligned dword and the +-1 neighbours'
+// direction bytes as one dword at v - 1 as well: neutral (one-byte loads are cheap; the 16-byte
+// ones fill the texture data path).
+#ifndef GP_CSR_VEC
+#define GP_CSR_VEC 1
+#endif
+constexpr bool kCsrVec = GP_CSR_VEC != 0 && kAblate == 0;
 // The quiet-wave round kernel's SGPR cap (GP_PSQ_SGPR, 0 = the compiler's choice).  A 256-thread
 // workgroup is admitted per CU only while 800 / (ceil(sgpr / 16) * 16 + 16) allows it
 // (MI355X_MICROARCH.md, residency): 106 SGPRs -> 6 workgroups, <= 96 -> 7, <= 80 -> 8.
@@ -374,6 +385,12 @@ __device__ __forceinline__ PsLevel1 ps_level1(const RoundArgs& a, const Geom& g,
             if (kAblate & 512u) {
                 p.li = v;
                 p.nl = 1u;
+            } else if constexpr (kCsrVec) {  // rev_off[v], rev_off[v + 1] in one 8-byte load
+                typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+                u2v o;
+                __builtin_memcpy(&o, &a.rev_off[v], sizeof o);
+                p.li = o.x;
+                p.nl = (kAblate & 1u) ? 0u : o.y - o.x;
             } else {
                 p.li = a.rev_off[v];
                 p.nl = (kAblate & 1u) ? 0u : a.rev_off[v + 1] - p.li;
@@ -458,15 +475,35 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
         };
         if (LM) {
             uint32_t ls[kLinkUnroll];
-#pragma unroll
-            for (uint32_t k = 0; k < kLinkUnroll; ++k)
-                ls[k] = ((kAblate & 2097152u) && k >= 2u) ? li + k : load_sel(a.rev_src, k < nl, ab<1024u>(li + k), a.slot_lo);
             bool lk[kLinkUnroll];
             double2 lm[kLinkUnroll];
             uint8_t lc[kLinkUnroll];
+            if constexpr (kCsrVec && kLinkUnroll == 4) {
+                // the four unrolled slots' sources as one 16-byte load and their marks as two
+                // aligned dwords (slots past nl belong to the next actors and are ignored; the
+                // arrays are padded past their last slot)
+                typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+                u4v s4;
+                __builtin_memcpy(&s4, &a.rev_src[li], sizeof s4);
+                ls[0] = s4.x;
+                ls[1] = s4.y;
+                ls[2] = s4.z;
+                ls[3] = s4.w;
+                const uint32_t* mw = reinterpret_cast<const uint32_t*>(a.lcnt_prev + (li & ~3u));
+                const uint64_t m8 = (uint64_t)mw[0] | ((uint64_t)mw[1] << 32);
+                const uint32_t sh = 8u * (li & 3u);
 #pragma unroll
-            for (uint32_t k = 0; k < kLinkUnroll; ++k)
-                lc[k] = ((kAblate & 2097152u) && k >= 2u) ? (uint8_t)(li >> 3) : load_sel(a.lcnt_prev, k < nl, ab<2048u>(li + k), a.slot_lo);
+                for (uint32_t k = 0; k < 4; ++k) lc[k] = (uint8_t)(m8 >> (sh + 8u * k));
+            } else {
+#pragma unroll
+                for (uint32_t k = 0; k < kLinkUnroll; ++k)
+                    ls[k] = ((kAblate & 2097152u) && k >= 2u) ? li + k
+                                                              : load_sel(a.rev_src, k < nl, ab<1024u>(li + k), a.slot_lo);
+#pragma unroll
+                for (uint32_t k = 0; k < kLinkUnroll; ++k)
+                    lc[k] = ((kAblate & 2097152u) && k >= 2u) ? (uint8_t)(li >> 3)
+                                                              : load_sel(a.lcnt_prev, k < nl, ab<2048u>(li + k), a.slot_lo);
+            }
             // ---- level 3: the messages of the sources whose slot is marked
 #pragma unroll
             for (uint32_t k = 0; k < kLinkUnroll; ++k)
