@@ -206,6 +206,19 @@ constexpr bool kMsgFallbackLo = GP_MSG_FALLBACK_LO != 0;
 #define GP_LINK_UNROLL 4
 #endif
 constexpr uint32_t kLinkUnroll = GP_LINK_UNROLL;
+// A converged actor's held-row load as a branch-free load of one shared row (1) or an
+// exec-masked load under a branch (0, A/B knob): C3 -1% (profiles/round3/held_ab).
+#ifndef GP_HELD_SEL
+#define GP_HELD_SEL 1
+#endif
+constexpr bool kHeldSel = GP_HELD_SEL != 0;
+// Message loads issued for an actor's first GP_GRID_LOADS grid hits (A/B knob); later hits are
+// loaded on demand.  2 instead of 3: neutral (profiles/round3/held_ab).
+#ifndef GP_GRID_LOADS
+#define GP_GRID_LOADS 3
+#endif
+constexpr uint32_t kGridLoads = GP_GRID_LOADS;
+static_assert(kGridLoads >= 1 && kGridLoads <= 6, "GP_GRID_LOADS: 1 .. 6");
 // One GPU: message loads issued for the first GP_FIRED_LOADS fired link slots of an actor, the
 // others on demand (GP_LINK_UNROLL: one per unrolled slot, fired or not).  1: C3 -3%, 100M -1%
 // against 4 (each predicated 16-byte load instruction costs ~1.5% of an all-sending round,
@@ -418,17 +431,17 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
 #pragma unroll
         for (uint32_t k = 0; k < 6; ++k) hits |= ((m & slot_bit(k)) && d[k] == slot_code(k)) ? 1u << k : 0u;
         if (kAblate & 16u) hits = 0;
-        // The first three grid hits (slot order = ascending source id) and their sources (none:
-        // above every bound), computed once for the loads and the merge.
-        uint32_t gs[3], rest = hits;
+        // The first kGridLoads grid hits (slot order = ascending source id) and their sources
+        // (none: above every bound), computed once for the loads and the merge.
+        uint32_t gs[kGridLoads], rest = hits;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
+        for (int j = 0; j < (int)kGridLoads; ++j) {
             gs[j] = slot_src(g, v, (uint32_t)__builtin_ctz(rest | 64u)) | (0u - (uint32_t)(rest == 0u));
             rest &= rest - 1u;
         }
-        double2 gm[3];
+        double2 gm[kGridLoads];
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
+        for (int j = 0; j < (int)kGridLoads; ++j)
             gm[j] = (PRE || ((kAblate & 1048576u) && j == 2)) ? make_double2(0.0, 0.0)
                         : load_sel(a.msg_prev, gs[j] != 0xFFFFFFFFu,
                                    (gs[j] == v - g.plane || gs[j] == v + g.plane) ? ab<32768u>(ab<16384u>(gs[j]))
@@ -438,7 +451,10 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
         // A converged actor only relays what arrives (program.fs:125-127): its held (S,W) and so
         // its message row are not read (more than half of the C3 run's actor-rounds).  Issued
         // with the second load level, when the flags byte has long arrived.
-        if (!PRE && kSkipConvHeld && !(f & 16u)) held = a.msg_prev[ab<64u>(v)];
+        if constexpr (!PRE && kSkipConvHeld && kHeldSel)
+            held = load_sel(a.msg_prev, !(f & 16u), ab<64u>(v), a.lo);
+        else if (!PRE && kSkipConvHeld && !(f & 16u))
+            held = a.msg_prev[ab<64u>(v)];
         uint32_t gi = 0;
         auto add = [&](double2 mm) {
             ss += mm.x;
@@ -458,12 +474,12 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                 return;
             }
 #pragma unroll
-            for (int j = 0; j < 3; ++j)
+            for (int j = 0; j < (int)kGridLoads; ++j)
                 if (gi == (uint32_t)j && gs[j] < bound) {
                     add(gm[j]);
                     ++gi;
                 }
-            if (gi >= 3) {
+            if (gi >= kGridLoads) {
                 while (rest) {
                     const uint32_t k = (uint32_t)__builtin_ctz(rest);
                     const uint32_t u = slot_src(g, v, k);
