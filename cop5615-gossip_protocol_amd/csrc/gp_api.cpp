@@ -151,7 +151,8 @@ struct Handle {
     int64_t total_cap = 0;
     uint32_t* parts = nullptr;
     double2* partials = nullptr;
-    unsigned long long* h_trace = nullptr;  // pinned
+    unsigned long long* h_trace = nullptr;  // pinned, host-mapped (coherent)
+    unsigned long long* d_trace = nullptr;  // its device address
     int64_t h_trace_cap = 0;
     int64_t next_kernel = 0;  // index of the next fused round kernel F(k)
     int64_t rounds = 0;       // rounds whose results are final
@@ -657,18 +658,21 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
             }
         }
         h->next_kernel += B;
-        // total[] of the last round this batch applied (F(k) applies round k, or k-1 for gossip)
-        launch_finalize(h->total, h->parts, h->next_kernel - (h->gossip ? 2 : 1), h->stream);
-        HIP_TRY(hipGetLastError());
-        // total[] entries of the rounds completed by this batch
+        // total[] of the last round this batch applied (F(k) applies round k, or k-1 for gossip),
+        // and the total[] entries of the rounds this batch completed, written by the same kernel
+        // into host-mapped memory (a device-to-host copy after it cost ~0.3 ms of queue time per
+        // batch: profiles/round3/c3/rocprof_kernel_stats_whole_run.csv, round 3)
         if (B > h->h_trace_cap) {
             if (h->h_trace) (void)hipHostFree(h->h_trace);
             h->h_trace = nullptr;
-            HIP_TRY(hipHostMalloc((void**)&h->h_trace, (size_t)B * sizeof(unsigned long long), 0));
+            h->d_trace = nullptr;
+            HIP_TRY(hipHostMalloc((void**)&h->h_trace, (size_t)B * sizeof(unsigned long long),
+                                  hipHostMallocMapped | hipHostMallocCoherent));
+            HIP_TRY(hipHostGetDevicePointer((void**)&h->d_trace, h->h_trace, 0));
             h->h_trace_cap = B;
         }
-        HIP_TRY(hipMemcpyAsync(h->h_trace, h->total + h->rounds, (size_t)B * sizeof(unsigned long long),
-                               hipMemcpyDeviceToHost, h->stream));
+        launch_finalize(h->total, h->parts, h->next_kernel - (h->gossip ? 2 : 1), h->stream, h->d_trace, h->rounds);
+        HIP_TRY(hipGetLastError());
         HIP_TRY(hipStreamSynchronize(h->stream));
         int64_t real = B;
         for (int64_t i = 0; i < B; ++i) {

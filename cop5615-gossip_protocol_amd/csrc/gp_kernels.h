@@ -232,7 +232,9 @@ size_t scan_scratch_words(uint32_t n);
 void launch_exclusive_scan(const uint32_t* in, uint32_t* off, uint32_t n, uint32_t* scratch, hipStream_t s);
 void launch_fill_u8(uint8_t* p, uint8_t v, size_t n, hipStream_t s);
 // total[a] = total[a-1] + sum of the round-a sub-counters (after the last kernel of a batch)
-void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hipStream_t s);
+// (out: also total[first .. a] into out[], e.g. host-mapped memory)
+void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hipStream_t s,
+                     unsigned long long* out = nullptr, long long first = 0);
 void launch_ps_init(uint8_t* flags, const Geom& g, uint32_t lo, uint32_t hi, uint32_t full, uint32_t term_init,
                     const Launch& l);
 // push-sum sums for gp_status: per-block partials of held + in-flight (s, w)

@@ -1653,11 +1653,17 @@ __global__ void k_fill_u8(uint8_t* p, uint8_t val, size_t n) {
 }
 
 
-__global__ void k_finalize(unsigned long long* total, uint32_t* parts, long long a) {
+// total[a] from the round-a sub-counters; with `out`, also total[first .. a] into out[0 ..
+// a - first] (host-mapped memory: the host reads the batch's counts without a copy).
+__global__ void k_finalize(unsigned long long* total, uint32_t* parts, long long a, unsigned long long* out,
+                           long long first) {
     unsigned long long x = *part_slot(parts, a, threadIdx.x);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-    if (threadIdx.x == 0) total[a] = x + (a >= 1 ? total[a - 1] : 0ull);
+    x += a >= 1 ? total[a - 1] : 0ull;
+    if (threadIdx.x == 0) total[a] = x;
+    if (out)
+        for (long long i = threadIdx.x; first + i <= a; i += 64) out[i] = first + i == a ? x : total[first + i];
 }
 
 __global__ void k_ps_init(uint8_t* flags, Geom g, uint32_t lo, uint32_t hi, uint32_t full, uint32_t term_init) {
@@ -1857,8 +1863,9 @@ void launch_fill_u8(uint8_t* p, uint8_t v, size_t n, hipStream_t s) {
 }
 
 
-void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hipStream_t s) {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, total, parts, a);
+void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hipStream_t s, unsigned long long* out,
+                     long long first) {
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, total, parts, a, out, first);
 }
 
 void launch_ps_init(uint8_t* flags, const Geom& g, uint32_t lo, uint32_t hi, uint32_t full, uint32_t term_init,
