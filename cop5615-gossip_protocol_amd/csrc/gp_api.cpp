@@ -561,6 +561,10 @@ int launch_aux(Handle* h, int64_t k, const Xchg* x) {
 }
 
 constexpr int64_t kTimeEvery = 8;  // kernel timing: one round in 8
+// Kernel timing without a pass after the round kernel: one event pair per group of kTimeGroup
+// consecutive rounds.  Each record stalls the queue: groups of 8 added 9.3 ms to a 129 ms C3
+// run (7%, and 40% of a 20 us tail round); groups of 64 add about 1/8 of that (round 3).
+constexpr int64_t kTimeGroup = 64;
 #ifndef GP_TAIL_BATCH
 #define GP_TAIL_BATCH 32
 #endif
@@ -642,17 +646,18 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
             h->next_kernel = 1;
         }
         // Kernel timing.  With no pass after the round kernel, one event pair brackets each group
-        // of kTimeEvery consecutive round kernels (per-launch time = group time / rounds, launch
+        // of kTimeGroup consecutive round kernels (per-launch time = group time / rounds, launch
         // gaps included); otherwise every kTimeEvery-th round is bracketed kernel by kernel.  Either
         // way the events stay out of most of the stream (each record costs stream time).
         const bool group = timing && aux_kernel_name(h)[0] == '\0';
-        const int64_t ng = (B + kTimeEvery - 1) / kTimeEvery;
+        const int64_t every = group ? kTimeGroup : kTimeEvery;
+        const int64_t ng = (B + every - 1) / every;
         if (timing && (rc = ensure_events(h, ng))) return rc;
         for (int64_t i = 0; i < B; ++i) {
-            const int64_t j = i / kTimeEvery;
-            if (group && i % kTimeEvery == 0) HIP_TRY(hipEventRecord(h->kev[3 * j], h->stream));
-            if ((rc = launch_round(h, h->next_kernel + i, nullptr, timing && !group && i % kTimeEvery == 0, j))) return rc;
-            if (group && (i % kTimeEvery == kTimeEvery - 1 || i == B - 1)) {
+            const int64_t j = i / every;
+            if (group && i % every == 0) HIP_TRY(hipEventRecord(h->kev[3 * j], h->stream));
+            if ((rc = launch_round(h, h->next_kernel + i, nullptr, timing && !group && i % every == 0, j))) return rc;
+            if (group && (i % every == every - 1 || i == B - 1)) {
                 HIP_TRY(hipEventRecord(h->kev[3 * j + 1], h->stream));
                 HIP_TRY(hipEventRecord(h->kev[3 * j + 2], h->stream));
             }
@@ -686,7 +691,7 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         h->rounds += real;
         if (group) {  // groups wholly inside the real rounds
             for (int64_t j = 0; j < ng; ++j) {
-                const int64_t first = j * kTimeEvery, last = std::min<int64_t>(first + kTimeEvery, B) - 1;
+                const int64_t first = j * every, last = std::min<int64_t>(first + every, B) - 1;
                 if (last >= real) break;
                 float ms = 0.f;
                 HIP_TRY(hipEventElapsedTime(&ms, h->kev[3 * j], h->kev[3 * j + 1]));
@@ -1101,8 +1106,8 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
             (h->g.actors >= kQuietMinActors || (cfg->flags & GP_FLAG_QUIET_WAVES))) {  // quiet-wave marks
             for (int i = 0; i < 2; ++i)
                 if ((rc = h->alloc(&h->act[i], act_bytes(h)))) return bail(rc);
-            if ((rc = h->alloc(&h->work, 1))) return bail(rc);
-            if (hipMemsetAsync(h->work, 0, sizeof *h->work, h->stream) != hipSuccess)
+            if ((rc = h->alloc(&h->work, (size_t)kParts * kWorkStride))) return bail(rc);
+            if (hipMemsetAsync(h->work, 0, (size_t)kParts * kWorkStride * sizeof *h->work, h->stream) != hipSuccess)
                 return bail(fail(GP_EHIP, "hipMemsetAsync failed"));
             h->act_thr = (uint32_t)((uint64_t)h->lay.nodes * GP_ACT_PCT / 100u);
         }
@@ -1663,17 +1668,20 @@ int gp_kernel_stats(void* handle, gp_kstats* out, int32_t reset_counters) {
     std::snprintf(out->aux_kernel, sizeof out->aux_kernel, "%s", aux_kernel_name(h));
     out->work_per_launch = (double)h->own();
     if (h->act[0] && h->work) {  // the quiet kernel counts the actors it walks
-        unsigned long long w = 0;
-        HIP_TRY(hipMemcpyAsync(&w, h->work, sizeof w, hipMemcpyDeviceToHost, h->stream));
+        std::vector<unsigned long long> w((size_t)kParts * kWorkStride);
+        HIP_TRY(hipMemcpyAsync(w.data(), h->work, w.size() * sizeof w[0], hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(hipStreamSynchronize(h->stream));
-        out->work_per_launch = h->work_rounds ? (double)w / (double)h->work_rounds : 0.0;
+        unsigned long long t = 0;
+        for (int i = 0; i < kParts; ++i) t += w[(size_t)i * kWorkStride];
+        out->work_per_launch = h->work_rounds ? (double)t / (double)h->work_rounds : 0.0;
     }
     if (reset_counters) {
         h->k_launches = 0;
         h->k_total_ms = 0.0;
         h->k_aux_ms = 0.0;
         h->work_rounds = 0;
-        if (h->work) HIP_TRY(hipMemsetAsync(h->work, 0, sizeof *h->work, h->stream));
+        if (h->work)
+            HIP_TRY(hipMemsetAsync(h->work, 0, (size_t)kParts * kWorkStride * sizeof *h->work, h->stream));
     }
     return GP_OK;
 }

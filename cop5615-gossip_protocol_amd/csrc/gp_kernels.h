@@ -18,6 +18,7 @@ constexpr int kMaxGrid = 256 * GP_GRID_PER_CU;
 constexpr int kParts = 64;          // completion sub-counters per round (one 64 B line each)
 constexpr int kPartStride = 16;     // u32 words between sub-counters
 constexpr int kPartRing = 4;        // rounds kept in the sub-counter ring
+constexpr int kWorkStride = 8;      // u64 words between the walked-actor sub-counters
 constexpr int kMaxWorld = 16;
 // Exchange entries to one peer are appended into kSub sub-segments (sub = blockIdx % kSub), each
 // with its own counter on its own 128 B line: same-address atomics serialise in L2 (measured at
@@ -112,7 +113,8 @@ struct RoundArgs {
     uint32_t* tgt_cur;        // destination of v's message (UINT32_MAX none)
     uint32_t* pos_cur;        // slot of v's message inside its destination bucket
     // kernel statistics (GP_FLAG_KERNEL_TIMING, one-GPU quiet kernel): actors walked, summed over
-    // launches; null: not counted
+    // launches into kParts sub-counters kWorkStride apart (one per workgroup slot: a single
+    // counter serialised 1792 atomics per round); null: not counted
     unsigned long long* work;
 };
 

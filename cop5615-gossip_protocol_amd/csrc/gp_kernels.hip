@@ -780,7 +780,7 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a) {
             }
         }
         block_add(newly, a.parts, r);
-        if (a.work) block_add_u64(walked, a.work);
+        if (a.work) block_add_u64(walked, a.work + (blockIdx.x & (kParts - 1)) * kWorkStride);
         return;
     }
     for (; v < end; v += step) {

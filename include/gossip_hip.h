@@ -43,7 +43,7 @@ enum gp_error {
 };
 
 enum gp_flags {
-    GP_FLAG_KERNEL_TIMING = 1, /* hipEvent kernel timing (gp_kernel_stats): gp_step brackets groups of 8 rounds (or every 8th kernel when a pass follows it); a shard brackets every 8th round */
+    GP_FLAG_KERNEL_TIMING = 1, /* hipEvent kernel timing (gp_kernel_stats): gp_step brackets groups of 64 rounds (or every 8th kernel when a pass follows it); a shard brackets every 8th round */
     GP_FLAG_GENERIC = 2,       /* force the generic bucketed push path on grid topologies    */
     GP_FLAG_USE_STREAM = 4,    /* run on cfg->stream even when it is NULL (the null stream)  */
     GP_FLAG_ONE_DEVICE = 8,    /* num_gpus > 1: every shard on cfg->device, exchange by device
