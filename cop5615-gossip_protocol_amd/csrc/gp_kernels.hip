@@ -227,6 +227,11 @@ static_assert(kGridLoads >= 1 && kGridLoads <= 6, "GP_GRID_LOADS: 1 .. 6");
 #define GP_FIRED_LOADS 1
 #endif
 constexpr uint32_t kFiredLoads = GP_FIRED_LOADS;
+// A/B knob: the shard round kernel (LM 2) loads fired links the same way (1) or per slot (0).
+#ifndef GP_FIRED_SHARDS
+#define GP_FIRED_SHARDS 0
+#endif
+constexpr bool kFiredShards = GP_FIRED_SHARDS != 0;
 
 // Timing-only builds (tools/variants) may drop parts of the round kernel to price them; the
 // product is built with 0, and the results of any other value are wrong by construction.
@@ -524,12 +529,18 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
 #pragma unroll
             for (uint32_t k = 0; k < kLinkUnroll; ++k)
                 lk[k] = k < nl && ((kAblate & 131072u) ? ls[k] % 7u == 0u : lc[k] == a.tag_prev);  // round tags
-            if constexpr (LM == 1 && kFiredLoads < kLinkUnroll) {
-                // one GPU: load the messages of the first kFiredLoads FIRED slots only (about one
-                // slot in seven fires: 0.14 messages per actor), the rest on demand (rare)
+            if constexpr (LM != 0 && kFiredLoads < kLinkUnroll && (LM == 1 || kFiredShards)) {
+                // load the messages of the first kFiredLoads FIRED slots only (about one slot in
+                // seven fires: 0.14 messages per actor), the rest on demand (rare).  A shard reads
+                // a remote source's message from the receiver's slot (rmsg_prev), a local one from
+                // the source's row: one load through a selected address.
                 uint32_t rest = 0;
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) rest |= lk[k] ? 1u << k : 0u;
+                auto msg_of = [&](uint32_t k, uint32_t u) -> const double2* {
+                    if (LM == 2 && (u < a.lo || u >= a.hi)) return a.rmsg_prev + (li + k);
+                    return a.msg_prev + ab<8192u>(u);
+                };
                 uint32_t fs[kFiredLoads];
                 bool fv[kFiredLoads];
                 double2 fm[kFiredLoads];
@@ -541,11 +552,9 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
 #pragma unroll
                     for (uint32_t q = 1; q < kLinkUnroll; ++q) u = k == q ? ls[q] : u;
                     fs[j] = u;
+                    fm[j] = *(fv[j] ? msg_of(k, u) : a.msg_prev + (kMsgFallbackLo ? a.lo : v));
                     rest &= rest - 1u;
                 }
-#pragma unroll
-                for (uint32_t j = 0; j < kFiredLoads; ++j)
-                    fm[j] = load_sel(a.msg_prev, fv[j], ab<8192u>(fs[j]), kMsgFallbackLo ? a.lo : v);
 #pragma unroll
                 for (uint32_t j = 0; j < kFiredLoads; ++j)
                     if (fv[j]) {
@@ -558,7 +567,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
 #pragma unroll
                     for (uint32_t q = 1; q < kLinkUnroll; ++q) u = k == q ? ls[q] : u;
                     flush(u);
-                    add(a.msg_prev[u]);
+                    add(*msg_of(k, u));
                     rest &= rest - 1u;
                 }
             } else {
