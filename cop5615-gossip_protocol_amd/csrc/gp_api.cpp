@@ -14,6 +14,13 @@
 #define GP_ACT_PCT 99
 #endif
 constexpr uint32_t kQuietMinActors = 1u << 20;
+// Full gossip on one GPU: the receipt tally (gp_kernels.h GsTally) is built from this many actors
+// and used in a round after one that emitted at least actors / kTallyThrDiv chains.
+constexpr size_t kTallyMinActors = 1u << 20;
+#ifndef GP_TALLY_THR_DIV
+#define GP_TALLY_THR_DIV 2
+#endif
+constexpr size_t kTallyThrDiv = GP_TALLY_THR_DIV;
 
 #include <algorithm>
 #include <chrono>
@@ -139,6 +146,7 @@ struct Handle {
     uint8_t* gstate = nullptr;
     uint32_t* inc[2] = {nullptr, nullptr};
     uint32_t* dbits = nullptr;  // full gossip on one GPU: done bitmap (k_gs_full4's sender filter)
+    GsTally tally{};            // full gossip on one GPU: receipt tally by target bucket (cnt null: off)
     // generic push-sum buckets
     uint32_t* bcnt[2] = {nullptr, nullptr};
     uint32_t* boff[2] = {nullptr, nullptr};
@@ -430,6 +438,11 @@ int reset(Handle* h) {
             HIP_TRY(hipMemsetAsync(h->inc[0] + lo, 0, n * sizeof(uint32_t), h->stream));
             HIP_TRY(hipMemsetAsync(h->inc[1] + lo, 0, n * sizeof(uint32_t), h->stream));
             if (h->dbits) HIP_TRY(hipMemsetAsync(h->dbits, 0, (n + 31) / 32 * sizeof(uint32_t), h->stream));
+            if (h->tally.cnt) {
+                HIP_TRY(hipMemsetAsync(h->tally.chains, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t),
+                                       h->stream));
+                HIP_TRY(hipMemsetAsync(h->tally.on, 0, 4 * sizeof(uint32_t), h->stream));
+            }
         } else {
             launch_fill_u8(h->dir[0] + xlo, 0xFF, xn, h->stream);
             launch_fill_u8(h->dir[1] + xlo, 0xFF, xn, h->stream);
@@ -525,7 +538,10 @@ void launch_main(Handle* h, int64_t k, const Xchg* x) {
     if (h->gossip) {
         if (h->generic) {  // adds into inc_cur, consumed (zeroed) by F(k+1)
             if (x) launch_gs_push_x(a, *x, l);
-            else if (full_quad(h)) launch_gs_full4(a, l);
+            else if (full_quad(h)) {
+                launch_gs_full4(a, h->tally, l);
+                launch_gs_tally(a, h->tally, l);
+            }
             else launch_gs_push(a, l);
         } else {
             launch_gs_pull(a, l);
@@ -1092,6 +1108,20 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
         if (h->generic) {
             if ((rc = h->alloc(&h->inc[0], n, lo)) || (rc = h->alloc(&h->inc[1], n, lo))) return bail(rc);
             if (full_quad(h) && (rc = h->alloc(&h->dbits, (n + 31) / 32))) return bail(rc);
+            const uint32_t nb = (uint32_t)((n + (1u << kTallyShift) - 1) >> kTallyShift);
+            if (full_quad(h) && nb <= kMaxTallyBuckets &&
+                (n >= kTallyMinActors || (cfg->flags & GP_FLAG_GOSSIP_TALLY))) {
+                GsTally& t = h->tally;
+                t.nb = nb;
+                t.W = (uint32_t)h->grid;
+                t.thr = (cfg->flags & GP_FLAG_GOSSIP_TALLY) ? 0u : (uint32_t)std::min<size_t>(n / kTallyThrDiv, 0xFFFFFFFFu);
+                const size_t nc = (size_t)nb * t.W;
+                if ((rc = h->alloc(&t.cnt, nc)) || (rc = h->alloc(&t.off, nc + 1)) || (rc = h->alloc(&t.tgt, 2 * n)) ||
+                    (rc = h->alloc(&t.scratch, scan_scratch_words((uint32_t)nc))) ||
+                    (rc = h->alloc(&t.chains, (size_t)kPartRing * kParts * kPartStride)) || (rc = h->alloc(&t.on, 4)))
+                    return bail(rc);
+                if (prepare_gs_tally()) return bail(fail(GP_EHIP, "hipFuncSetAttribute (tally LDS) failed"));
+            }
         } else if ((rc = h->alloc(&h->dir[0], xn, xlo)) || (rc = h->alloc(&h->dir[1], xn, xlo))) {
             return bail(rc);
         }

@@ -204,7 +204,28 @@ void launch_link_count(const RoundArgs& a, const Launch& l);
 void launch_ps_push_emit(const RoundArgs& a, const Launch& l);
 void launch_ps_push_fill(const RoundArgs& a, uint32_t* slot_cur, const uint32_t* boff_cur, const Launch& l);
 void launch_gs_push(const RoundArgs& a, const Launch& l);
-void launch_gs_full4(const RoundArgs& a, const Launch& l);  // full gossip, one GPU (lo == 0)
+// Full gossip on one GPU: receipt tally by target bucket.  In a round that follows
+// one with at least `thr` emitted chains, k_gs_full4 counts its receipts per (target bucket,
+// workgroup) in LDS instead of adding each with a memory-side atomic; a scan of those counts, a
+// scatter of the receipts by bucket (the draws recomputed) and an LDS tally per bucket then write
+// inc_cur whole.  Receipts to done targets are not filtered there (the receiver drops them).
+constexpr uint32_t kTallyShift = 15;          // 32768 targets per bucket: 128 KB of LDS counters
+constexpr uint32_t kMaxTallyBuckets = 4096;   // k_gs_full4's LDS counters: 16 KB at most
+struct GsTally {
+    uint32_t* cnt;     // [nb * W] receipts per (bucket, workgroup), bucket-major; null: no tally
+    uint32_t* off;     // [nb * W + 1] exclusive scan of cnt
+    uint32_t* tgt;     // receipts grouped by bucket (2 per actor at most)
+    uint32_t* scratch; // scan scratch (scan_scratch_words(nb * W))
+    uint32_t* chains;  // [4][kParts * kPartStride]: chains emitted in round r, ring slot r & 3
+    uint32_t* on;      // [4]: round r tallies (written by block 0 of F(r))
+    uint32_t thr;      // tally in round r >= 1 when round r - 1 emitted at least thr chains to
+                       // targets not done yet (estimated from the share of nodes not done)
+    uint32_t nb, W;    // buckets; k_gs_full4's grid
+};
+void launch_gs_full4(const RoundArgs& a, const GsTally& t, const Launch& l);  // full gossip, one GPU (lo == 0)
+// the scan, scatter and tally passes of a tallied round (each exits at once otherwise)
+void launch_gs_tally(const RoundArgs& a, const GsTally& t, const Launch& l);
+int prepare_gs_tally();  // once per process: allow the tally pass's 128 KB of dynamic LDS (0: ok)
 // sharded variants: remote link / full-topology messages go to the send chunks of x
 void launch_ps_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);
 void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);

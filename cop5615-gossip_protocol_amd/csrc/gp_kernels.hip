@@ -1389,12 +1389,31 @@ __global__ __launch_bounds__(kBlock) void k_gs_push_x(RoundArgs a, Xchg x) { gs_
 #ifndef GP_GS_FILTER_DIV
 #define GP_GS_FILTER_DIV 16
 #endif
-__global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a) {
+// Chains emitted in round r (sum of the 64 sub-counters of ring slot r & 3), computed by every
+// wave for itself: all waves read the same final values.
+__device__ __forceinline__ uint32_t tally_chains(const GsTally& t, uint32_t r) {
+    return wave_sum(*part_slot(t.chains, r, threadIdx.x & 63u));
+}
+
+__global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
+    extern __shared__ uint32_t tcnt[];  // tally rounds: receipts per target bucket (t.nb)
     const uint32_t r = a.r;
     unsigned long long prev = 0;
-    if (r) {
-        prev = gate_count(a, (long long)r - 1);
-        if (prev >= a.target) return;
+    if (r) prev = gate_count(a, (long long)r - 1);
+    // tally this round: the previous one emitted at least thr chains (uniform: every block reads
+    // the same final counts); block 0 records the choice for the passes after this kernel
+    // (the chains of round r - 1 that reach a target not done yet: the atomics round r would issue,
+    // estimated from the share of nodes not done)
+    const bool tally = t.cnt && r >= 1u && prev < a.target &&
+                       (double)tally_chains(t, r - 1u) * (double)(a.target - prev) >= (double)t.thr * (double)a.target;
+    if (t.cnt && blockIdx.x == 0 && threadIdx.x < 64) {
+        *part_slot(t.chains, r + 2u, threadIdx.x) = 0u;  // the slot round r + 2 adds into
+        if (threadIdx.x == 0) t.on[r & 3u] = tally ? 1u : 0u;
+    }
+    if (r && prev >= a.target) return;
+    if (tally) {
+        for (uint32_t i = threadIdx.x; i < t.nb; i += kBlock) tcnt[i] = 0u;
+        __syncthreads();
     }
     const bool filter = (unsigned long long)GP_GS_FILTER_DIV * prev >= a.target;
     const uint32_t na = a.hi;  // one GPU: actors [0, na)
@@ -1402,7 +1421,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a) {
     const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;
     uint32_t q, end, step;
     node_range(0u, nq, span4, q, end, step);
-    uint32_t newly = 0;
+    uint32_t newly = 0, chains = 0;
     // uniform per wave: the 8 lanes sharing a bitmap word reduce together
     for (; q - (threadIdx.x & 63u) < end; q += step) {
         const bool valid = q < end;
@@ -1451,6 +1470,12 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a) {
                     const uint32_t t0 = scale_draw(px.x, a.nodes), u0 = t0 + (t0 >= v ? 1u : 0u);
                     const uint32_t t1 = scale_draw(px.y, a.nodes), u1 = t1 + (t1 >= v ? 1u : 0u);
                     const bool s1 = tok > 1;
+                    chains += s1 ? 2u : 1u;
+                    if (tally) {  // counted per target bucket (LDS); placed by k_gs_tally_scatter
+                        atomicAdd(&tcnt[u0 >> kTallyShift], 1u);
+                        if (s1) atomicAdd(&tcnt[u1 >> kTallyShift], 1u);
+                        continue;
+                    }
                     uint32_t b0 = 0, b1 = 0;
                     if (filter) {
                         b0 = a.dbits[u0 >> 5];
@@ -1469,6 +1494,69 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a) {
         if (w && (q & 7u) == 0u) atomicOr(&a.dbits[q >> 3], w);
     }
     if (r) block_add(newly, a.parts, (long long)r - 1);
+    if (t.cnt) {
+        __syncthreads();  // block_add's LDS slots are reused
+        block_add(chains, t.chains, r);
+    }
+    if (tally) {  // this workgroup's counts, bucket-major for the scan
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < t.nb; i += kBlock) t.cnt[i * t.W + blockIdx.x] = tcnt[i];
+    }
+}
+
+// Tallied round: place every receipt of F(r) into its bucket's segment, at this workgroup's
+// offset (the scan of k_gs_full4's counts) plus an LDS position.  Same grid and walk as
+// k_gs_full4, same draws, read from the states F(r) wrote, so each (bucket, workgroup) gets
+// exactly the count F(r) reported.
+__global__ __launch_bounds__(kBlock) void k_gs_tally_scatter(RoundArgs a, GsTally t) {
+    extern __shared__ uint32_t tpos[];
+    const uint32_t r = a.r;
+    if (!t.on[r & 3u]) return;  // uniform
+    // this workgroup's first position in every bucket's segment (then LDS atomics give each
+    // receipt its place without another global read)
+    for (uint32_t i = threadIdx.x; i < t.nb; i += kBlock) tpos[i] = t.off[i * t.W + blockIdx.x];
+    __syncthreads();
+    const uint32_t na = a.hi;
+    const uint32_t nq = (na + 3u) >> 2;
+    const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;
+    uint32_t q, end, step;
+    node_range(0u, nq, span4, q, end, step);
+    for (; q < end; q += step) {
+        const uint32_t v0 = q << 2;
+        const uint32_t st4 = *reinterpret_cast<const uint32_t*>(a.gstate + v0);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t v = v0 + j, tok = (st4 >> (8u * j)) & 3u;
+            if (tok && v < na) {
+                const uint4 px = philox(v, r, kStreamGossip, a.seed);
+                const uint32_t t0 = scale_draw(px.x, a.nodes), u0 = t0 + (t0 >= v ? 1u : 0u);
+                const uint32_t b0 = u0 >> kTallyShift;
+                t.tgt[atomicAdd(&tpos[b0], 1u)] = u0;
+                if (tok > 1) {
+                    const uint32_t t1 = scale_draw(px.y, a.nodes), u1 = t1 + (t1 >= v ? 1u : 0u);
+                    const uint32_t b1 = u1 >> kTallyShift;
+                    t.tgt[atomicAdd(&tpos[b1], 1u)] = u1;
+                }
+            }
+        }
+    }
+}
+
+// Tallied round: one workgroup per target bucket counts its receipts in LDS and writes the
+// bucket's whole range of inc_cur (zeros included, so nothing is left to clear).
+__global__ __launch_bounds__(kBlock) void k_gs_tally_count(RoundArgs a, GsTally t) {
+    extern __shared__ uint32_t h[];
+    if (!t.on[a.r & 3u]) return;  // uniform
+    constexpr uint32_t S = 1u << kTallyShift;
+    for (uint32_t i = threadIdx.x; i < S; i += kBlock) h[i] = 0u;
+    __syncthreads();
+    const uint32_t b = blockIdx.x;
+    const uint32_t s0 = t.off[b * t.W], s1 = t.off[(b + 1u) * t.W];
+    for (uint32_t i = s0 + threadIdx.x; i < s1; i += kBlock) atomicAdd(&h[t.tgt[i] & (S - 1u)], 1u);
+    __syncthreads();
+    const uint32_t base = b << kTallyShift, na = a.hi;
+    const uint32_t n = na - base < S ? na - base : S;
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) a.inc_cur[base + i] = h[i];
 }
 
 // Push-sum on any topology (used for "full"): messages are bucketed by destination with an
@@ -1610,7 +1698,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t& total)
     return base + inc - x;
 }
 
-__global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* in, uint32_t n, uint32_t* sums) {
+__global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* in, uint32_t n, uint32_t* sums,
+                                                         const uint32_t* gate) {
+    if (gate && !*gate) return;
     const uint32_t b0 = blockIdx.x * kScanTile;
     uint32_t s = 0;
     for (uint32_t i = threadIdx.x; i < kScanTile; i += kBlock) {
@@ -1622,7 +1712,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* in, uint
     if (threadIdx.x == 0) sums[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(kBlock) void k_scan_top(uint32_t* sums, uint32_t nb) {
+__global__ __launch_bounds__(kBlock) void k_scan_top(uint32_t* sums, uint32_t nb, const uint32_t* gate) {
+    if (gate && !*gate) return;
     uint32_t carry = 0;
     for (uint32_t b = 0; b < nb; b += kBlock) {
         const uint32_t i = b + threadIdx.x;
@@ -1635,7 +1726,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_top(uint32_t* sums, uint32_t nb
 }
 
 __global__ __launch_bounds__(kBlock) void k_scan_apply(const uint32_t* in, uint32_t* off, uint32_t n,
-                                                        const uint32_t* sums) {
+                                                        const uint32_t* sums, const uint32_t* gate) {
+    if (gate && !*gate) return;
     const uint32_t b0 = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
     uint32_t vals[kScanPer];
     uint32_t s = 0;
@@ -1782,8 +1874,28 @@ void launch_ps_push_fill(const RoundArgs& a, uint32_t* slot_cur, const uint32_t*
     hipLaunchKernelGGL(k_ps_push_fill, dim3(l.grid), dim3(kBlock), 0, l.stream, a, slot_cur, boff_cur);
 }
 
-void launch_gs_full4(const RoundArgs& a, const Launch& l) {
-    hipLaunchKernelGGL(k_gs_full4, dim3(l.grid), dim3(kBlock), 0, l.stream, a);
+void launch_gs_full4(const RoundArgs& a, const GsTally& t, const Launch& l) {
+    const unsigned lds = t.cnt ? t.nb * (unsigned)sizeof(uint32_t) : 0u;
+    hipLaunchKernelGGL(k_gs_full4, dim3(t.cnt ? t.W : (uint32_t)l.grid), dim3(kBlock), lds, l.stream, a, t);
+}
+
+int prepare_gs_tally() {
+    // the per-bucket tally keeps 32768 u32 counters (128 KB) in LDS
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gs_tally_count),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)((1u << kTallyShift) * sizeof(uint32_t))) == hipSuccess ? 0 : -1;
+}
+
+void launch_gs_tally(const RoundArgs& a, const GsTally& t, const Launch& l) {
+    if (!t.cnt || !a.r) return;
+    const uint32_t* gate = t.on + (a.r & 3u);
+    const uint32_t n = t.nb * t.W, nb = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kBlock), 0, l.stream, t.cnt, n, t.scratch, gate);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, l.stream, t.scratch, nb, gate);
+    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kBlock), 0, l.stream, t.cnt, t.off, n, t.scratch, gate);
+    hipLaunchKernelGGL(k_gs_tally_scatter, dim3(t.W), dim3(kBlock), t.nb * (unsigned)sizeof(uint32_t), l.stream, a, t);
+    hipLaunchKernelGGL(k_gs_tally_count, dim3(t.nb), dim3(kBlock), (1u << kTallyShift) * (unsigned)sizeof(uint32_t),
+                       l.stream, a, t);
 }
 
 void launch_gs_push(const RoundArgs& a, const Launch& l) {
@@ -1859,9 +1971,10 @@ size_t scan_scratch_words(uint32_t n) { return (n + kScanTile - 1) / kScanTile +
 void launch_exclusive_scan(const uint32_t* in, uint32_t* off, uint32_t n, uint32_t* scratch, hipStream_t s) {
     const uint32_t nb = (n + kScanTile - 1) / kScanTile;
     if (nb == 0) return;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kBlock), 0, s, in, n, scratch);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, s, scratch, nb);
-    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kBlock), 0, s, in, off, n, scratch);
+    const uint32_t* gate = nullptr;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kBlock), 0, s, in, n, scratch, gate);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, s, scratch, nb, gate);
+    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kBlock), 0, s, in, off, n, scratch, gate);
 }
 
 void launch_fill_u8(uint8_t* p, uint8_t v, size_t n, hipStream_t s) {

@@ -22,6 +22,7 @@ FLAG_USE_STREAM = 4
 FLAG_ONE_DEVICE = 8
 FLAG_GROUP = 16
 FLAG_QUIET_WAVES = 32
+FLAG_GOSSIP_TALLY = 64
 ERRORS = {-1: "GP_EINVAL", -2: "GP_ENOMEM", -3: "GP_EHIP", -4: "GP_ESTATE", -5: "GP_EOVERFLOW", -6: "GP_ERCCL"}
 
 

@@ -51,6 +51,9 @@ enum gp_flags {
     GP_FLAG_GROUP = 16,        /* use the multi-GPU engine (shards + RCCL) also at num_gpus = 1 */
     GP_FLAG_QUIET_WAVES = 32,  /* push-sum, one GPU: skip quiet waves at any graph
                                   size (default: from 2^20 actors on); a test hook, same results */
+    GP_FLAG_GOSSIP_TALLY = 64, /* full gossip, one GPU: tally receipts by target bucket in every
+                                  round from round 1 at any graph size (default: from 2^20 actors,
+                                  after a round with many chains); a test hook, same results */
 };
 
 typedef struct gp_config {

@@ -281,3 +281,24 @@ def test_quiet_work_count_vs_oracle():
     assert ks["work_per_launch"] < actors
     gpu.close()
     cpu.close()
+
+
+@pytest.mark.parametrize("n,seed", [(1000, 3), (70000, 5), (300000, 2), (1_200_000, 4)])
+def test_full_gossip_tally_vs_oracle(n, seed):
+    """Full gossip with the receipt tally by target bucket forced in every round from round 1
+    (GP_FLAG_GOSSIP_TALLY; by default it runs from 2^20 actors after a round with many chains):
+    the same trace and state as the oracle, bit for bit (receipts to done targets are counted
+    there and dropped by the receiver, instead of being filtered by the sender)."""
+    gpu = Simulator(n, "full", "gossip", seed=seed, gossip_tally=True)
+    cpu = oracle.OracleSim(n, "full", "gossip", seed=seed)
+    gs = gpu.step()
+    cs = cpu.step(threads=16)
+    assert gs.converged and (gs.round, gs.completed) == (cs.round, cs.completed)
+    np.testing.assert_array_equal(gpu.read_trace(), cpu.read_trace())
+    check_same(gpu, cpu, "gossip")
+    gpu.reset()  # a second run after a reset: the tally's ring counters start clean
+    gs2 = gpu.step()
+    assert (gs2.round, gs2.completed) == (cs.round, cs.completed)
+    np.testing.assert_array_equal(gpu.read_trace(), cpu.read_trace())
+    gpu.close()
+    cpu.close()
