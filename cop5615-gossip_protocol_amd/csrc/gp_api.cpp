@@ -14,6 +14,10 @@
 #define GP_ACT_PCT 99
 #endif
 constexpr uint32_t kQuietMinActors = 1u << 20;
+// Full gossip done bitmap: one bit per actor, then its summary (one bit per 32-actor word).
+inline size_t dbits_words(size_t n) { return (n + 31) / 32; }
+constexpr uint32_t kDsumMinActors = 1u << 25;  // the summary is used from here (dbits > an L2)
+inline size_t dbits_alloc_words(size_t n) { return dbits_words(n) + (dbits_words(n) + 31) / 32; }
 // Full gossip on one GPU: the receipt tally (gp_kernels.h GsTally) is built from this many actors
 // and used in a round after one that emitted at least actors / kTallyThrDiv chains.
 constexpr size_t kTallyMinActors = 1u << 20;
@@ -260,6 +264,7 @@ struct Handle {
             a.act_cur = act[(r + 1u) & 1u];
         }
         a.dbits = dbits;
+        a.dsum = dbits && own() >= kDsumMinActors ? dbits + dbits_words(own()) : nullptr;
         a.inc_prev = inc[p];
         a.inc_cur = inc[c];
         a.bcnt_prev = bcnt[p];
@@ -437,7 +442,7 @@ int reset(Handle* h) {
         if (h->generic) {
             HIP_TRY(hipMemsetAsync(h->inc[0] + lo, 0, n * sizeof(uint32_t), h->stream));
             HIP_TRY(hipMemsetAsync(h->inc[1] + lo, 0, n * sizeof(uint32_t), h->stream));
-            if (h->dbits) HIP_TRY(hipMemsetAsync(h->dbits, 0, (n + 31) / 32 * sizeof(uint32_t), h->stream));
+            if (h->dbits) HIP_TRY(hipMemsetAsync(h->dbits, 0, dbits_alloc_words(n) * sizeof(uint32_t), h->stream));
             if (h->tally.cnt) {
                 HIP_TRY(hipMemsetAsync(h->tally.chains, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t),
                                        h->stream));
@@ -1107,7 +1112,7 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
         if ((rc = h->alloc(&h->cnt, n, lo)) || (rc = h->alloc(&h->gstate, n, lo))) return bail(rc);
         if (h->generic) {
             if ((rc = h->alloc(&h->inc[0], n, lo)) || (rc = h->alloc(&h->inc[1], n, lo))) return bail(rc);
-            if (full_quad(h) && (rc = h->alloc(&h->dbits, (n + 31) / 32))) return bail(rc);
+            if (full_quad(h) && (rc = h->alloc(&h->dbits, dbits_alloc_words(n)))) return bail(rc);
             const uint32_t nb = (uint32_t)((n + (1u << kTallyShift) - 1) >> kTallyShift);
             if (full_quad(h) && nb <= kMaxTallyBuckets &&
                 (n >= kTallyMinActors || (cfg->flags & GP_FLAG_GOSSIP_TALLY))) {

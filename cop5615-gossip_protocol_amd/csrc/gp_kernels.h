@@ -103,6 +103,7 @@ struct RoundArgs {
         };
     };
     uint32_t* dbits;          // full gossip, one GPU: done bitmap (sender-side filter)
+    uint32_t* dsum;           // its summary: bit w set once word w of dbits is all ones
     uint32_t* inc_prev;       // generic path: receipts of round r-1 (atomics)
     uint32_t* inc_cur;
     // generic push-sum buckets (ping-pong)
