@@ -74,6 +74,19 @@ def test_cli_argument_contract():
     assert r.returncode == 2  # unknown option
 
 
+def test_kstats_struct_layout():
+    """gp_kstats as the header lays it out (ABI 4 appended work_per_launch), field by field."""
+    import ctypes as C
+
+    text = open(_abi.HEADER).read()
+    body = re.search(r"typedef struct gp_kstats \{(.*?)\} gp_kstats;", text, re.S).group(1)
+    names = re.findall(r"^\s*(?:int64_t|double|char)\s+(\w+)", body, re.M)
+    assert names == [f[0] for f in _abi.KStats._fields_] == [
+        "launches", "total_ms", "avg_ms", "bytes_per_launch", "kernel", "aux_avg_ms", "aux_kernel", "work_per_launch"]
+    assert _abi.KStats.work_per_launch.offset == 168 and C.sizeof(_abi.KStats) == 176
+    assert _abi.ABI_VERSION == 4 and re.search(r"#define GP_ABI_VERSION 4\b", text)
+
+
 def test_config_struct_layout():
     """gp_config as the header lays it out (ABI 3: num_gpus in the former reserved slot), so a
     P/Invoke / ctypes mirror built from the header agrees field by field."""
