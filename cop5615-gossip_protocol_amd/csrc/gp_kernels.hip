@@ -1559,21 +1559,148 @@ __global__ __launch_bounds__(kBlock) void k_gs_tally_scatter(RoundArgs a, GsTall
     }
 }
 
+// The receipts of actors v0 .. v0+3 in round r (the draws of k_gs_full4), one emit(u) each.
+template <class F>
+__device__ __forceinline__ void gs_draws4(const RoundArgs& a, uint32_t r, uint32_t v0, uint32_t st4, uint32_t na,
+                                          F&& emit) {
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t v = v0 + j, tok = (st4 >> (8u * j)) & 3u;
+        if (tok && v < na) {
+            const uint4 px = philox(v, r, kStreamGossip, a.seed);
+            const uint32_t t0 = scale_draw(px.x, a.nodes);
+            emit(t0 + (t0 >= v ? 1u : 0u));
+            if (tok > 1) {
+                const uint32_t t1 = scale_draw(px.y, a.nodes);
+                emit(t1 + (t1 >= v ? 1u : 0u));
+            }
+        }
+    }
+}
+
+// Exclusive scan of one u32 per thread over a workgroup of NT threads (wsum: NT / 64 words).
+template <uint32_t NT>
+__device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t x, uint32_t* wsum) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off, 64);
+        if (lane >= (uint32_t)off) inc += y;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < NT / 64; ++i)
+        if (i < w) base += wsum[i];
+    __syncthreads();
+    return base + inc - x;
+}
+
+// Tallied round, batched placement: a workgroup of kScatK x 256 threads walks the actors of
+// k_gs_full4's workgroups kScatK*s .. kScatK*s + kScatK - 1 (their segments of every bucket are
+// adjacent, so it fills them as one), in batches of as many walk iterations as its LDS holds.  A
+// batch is drawn twice: once to count its receipts per bucket, once to sort them by bucket in LDS;
+// then consecutive lanes store consecutive receipts of a bucket.  k_gs_tally_scatter stores each
+// receipt where its LDS position falls, one 4-byte store per line: its 98M receipts per C4 peak
+// round wrote 2.94 GB (7.5x the receipt bytes, profiles/round3/c4_tally/pmc_scatter.txt).
+constexpr uint32_t kScatK = 4;
+constexpr uint32_t kScatBlock = kScatK * kBlock;
+constexpr uint32_t kScatMaxPerIter = kScatBlock * 8u;  // 4 actors x 2 chains per thread
+__global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a, GsTally t, uint32_t cap) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t r = a.r;
+    if (!t.on[r & 3u]) return;  // uniform
+    const uint32_t nb = t.nb, W = t.W, tid = threadIdx.x;
+    uint32_t* tpos = lds;             // next position in each bucket's segment
+    uint32_t* hs = lds + nb;          // batch counts -> starts -> ends per bucket
+    uint32_t* misc = lds + 2u * nb;   // [0]: batch total; [16, 32): scan wave sums
+    uint32_t* S = misc + 32;          // the batch's receipts, bucket-sorted
+    for (uint32_t i = tid; i < nb; i += kScatBlock) tpos[i] = t.off[i * W + kScatK * blockIdx.x];
+    // this thread's walk: node_range of k_gs_full4 workgroup w, thread lt
+    const uint32_t w = kScatK * blockIdx.x + (tid >> 8), lt = tid & (kBlock - 1u);
+    const uint32_t na = a.hi, nq = (na + 3u) >> 2;
+    const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;
+    const uint32_t base = (w & 7u) * span4, step = (W >> 3) * kBlock;
+    const uint32_t end = base >= nq ? 0u : (base + span4 < nq ? base + span4 : nq);
+    const uint32_t q0 = base + (w >> 3) * kBlock + lt;
+    const uint32_t iters = (span4 + step - 1u) / step;
+    for (uint32_t it = 0; it < iters;) {  // uniform
+        for (uint32_t i = tid; i < nb; i += kScatBlock) hs[i] = 0u;
+        if (tid == 0) misc[0] = 0u;
+        __syncthreads();
+        uint32_t it1 = it, total = 0;
+        do {  // count: add iterations while one more cannot overflow S
+            const uint32_t q = q0 + it1 * step;
+            uint32_t c = 0;
+            if (q < end)
+                gs_draws4(a, r, q << 2, *reinterpret_cast<const uint32_t*>(a.gstate + (q << 2)), na, [&](uint32_t u) {
+                    atomicAdd(&hs[u >> kTallyShift], 1u);
+                    ++c;
+                });
+            c = wave_sum(c);
+            if ((tid & 63u) == 0) atomicAdd(&misc[0], c);
+            ++it1;
+            __syncthreads();
+            total = misc[0];
+            __syncthreads();
+        } while (it1 < iters && total + kScatMaxPerIter <= cap);
+        {  // starts: exclusive scan of the counts, 4 buckets per thread (nb <= 4 * kScatBlock)
+            uint32_t v[4], s = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t b = 4u * tid + j;
+                v[j] = b < nb ? hs[b] : 0u;
+                s += v[j];
+            }
+            uint32_t run = block_excl_scan_n<kScatBlock>(s, misc + 16);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t b = 4u * tid + j;
+                if (b < nb) hs[b] = run;
+                run += v[j];
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = it; i < it1; ++i) {  // sort: the same draws, placed by bucket
+            const uint32_t q = q0 + i * step;
+            if (q < end)
+                gs_draws4(a, r, q << 2, *reinterpret_cast<const uint32_t*>(a.gstate + (q << 2)), na,
+                          [&](uint32_t u) { S[atomicAdd(&hs[u >> kTallyShift], 1u)] = u; });
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < total; i += kScatBlock) {  // hs[b] now ends bucket b's run
+            const uint32_t u = S[i], b = u >> kTallyShift;
+            t.tgt[tpos[b] + i - (b ? hs[b - 1u] : 0u)] = u;
+        }
+        __syncthreads();
+        for (uint32_t b = tid; b < nb; b += kScatBlock) tpos[b] += hs[b] - (b ? hs[b - 1u] : 0u);
+        __syncthreads();
+        it = it1;
+    }
+}
+
 // Tallied round: one workgroup per target bucket counts its receipts in LDS and writes the
-// bucket's whole range of inc_cur (zeros included, so nothing is left to clear).
-__global__ __launch_bounds__(kBlock) void k_gs_tally_count(RoundArgs a, GsTally t) {
+// bucket's whole range of inc_cur (zeros included, so nothing is left to clear).  Its 128 KB of LDS
+// admit one workgroup per CU: GP_COUNT_BLOCK threads (A/B knob) keep that many in flight.
+#ifndef GP_COUNT_BLOCK
+#define GP_COUNT_BLOCK 1024
+#endif
+constexpr uint32_t kCountBlock = GP_COUNT_BLOCK;
+__global__ __launch_bounds__(kCountBlock) void k_gs_tally_count(RoundArgs a, GsTally t) {
     extern __shared__ uint32_t h[];
     if (!t.on[a.r & 3u]) return;  // uniform
     constexpr uint32_t S = 1u << kTallyShift;
-    for (uint32_t i = threadIdx.x; i < S; i += kBlock) h[i] = 0u;
+    for (uint32_t i = threadIdx.x; i < S; i += kCountBlock) h[i] = 0u;
     __syncthreads();
     const uint32_t b = blockIdx.x;
     const uint32_t s0 = t.off[b * t.W], s1 = t.off[(b + 1u) * t.W];
-    for (uint32_t i = s0 + threadIdx.x; i < s1; i += kBlock) atomicAdd(&h[t.tgt[i] & (S - 1u)], 1u);
+    for (uint32_t i = s0 + threadIdx.x; i < s1; i += kCountBlock) atomicAdd(&h[t.tgt[i] & (S - 1u)], 1u);
     __syncthreads();
     const uint32_t base = b << kTallyShift, na = a.hi;
     const uint32_t n = na - base < S ? na - base : S;
-    for (uint32_t i = threadIdx.x; i < n; i += kBlock) a.inc_cur[base + i] = h[i];
+    for (uint32_t i = threadIdx.x; i < n; i += kCountBlock) a.inc_cur[base + i] = h[i];
 }
 
 // Push-sum on any topology (used for "full"): messages are bucketed by destination with an
@@ -1896,11 +2023,23 @@ void launch_gs_full4(const RoundArgs& a, const GsTally& t, const Launch& l) {
     hipLaunchKernelGGL(k_gs_full4, dim3(t.cnt ? t.W : (uint32_t)l.grid), dim3(kBlock), lds, l.stream, a, t);
 }
 
+// Batched placement (k_gs_tally_scatter_lds, 1) or one store per receipt (0, A/B knob).
+#ifndef GP_SCATTER_LDS
+#define GP_SCATTER_LDS 1
+#endif
+constexpr uint32_t kScatLdsBytes = 160u * 1024u;  // one workgroup per CU
+bool g_scatter_lds = false;
+
 int prepare_gs_tally() {
     // the per-bucket tally keeps 32768 u32 counters (128 KB) in LDS
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gs_tally_count),
-                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)((1u << kTallyShift) * sizeof(uint32_t))) == hipSuccess ? 0 : -1;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gs_tally_count), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)((1u << kTallyShift) * sizeof(uint32_t))) != hipSuccess)
+        return -1;
+    g_scatter_lds = GP_SCATTER_LDS != 0 &&
+                    hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gs_tally_scatter_lds),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScatLdsBytes) == hipSuccess;
+    (void)hipGetLastError();
+    return 0;
 }
 
 void launch_gs_tally(const RoundArgs& a, const GsTally& t, const Launch& l) {
@@ -1910,8 +2049,12 @@ void launch_gs_tally(const RoundArgs& a, const GsTally& t, const Launch& l) {
     hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kBlock), 0, l.stream, t.cnt, n, t.scratch, gate);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, l.stream, t.scratch, nb, gate);
     hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kBlock), 0, l.stream, t.cnt, t.off, n, t.scratch, gate);
-    hipLaunchKernelGGL(k_gs_tally_scatter, dim3(t.W), dim3(kBlock), t.nb * (unsigned)sizeof(uint32_t), l.stream, a, t);
-    hipLaunchKernelGGL(k_gs_tally_count, dim3(t.nb), dim3(kBlock), (1u << kTallyShift) * (unsigned)sizeof(uint32_t),
+    const uint32_t cap = kScatLdsBytes / 4u - 2u * t.nb - 32u;
+    if (g_scatter_lds && t.W % kScatK == 0 && t.nb <= 4u * kScatBlock && cap >= kScatMaxPerIter)
+        hipLaunchKernelGGL(k_gs_tally_scatter_lds, dim3(t.W / kScatK), dim3(kScatBlock), kScatLdsBytes, l.stream, a, t, cap);
+    else
+        hipLaunchKernelGGL(k_gs_tally_scatter, dim3(t.W), dim3(kBlock), t.nb * (unsigned)sizeof(uint32_t), l.stream, a, t);
+    hipLaunchKernelGGL(k_gs_tally_count, dim3(t.nb), dim3(kCountBlock), (1u << kTallyShift) * (unsigned)sizeof(uint32_t),
                        l.stream, a, t);
 }
 
