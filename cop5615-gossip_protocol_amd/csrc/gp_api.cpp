@@ -19,10 +19,12 @@ inline size_t dbits_words(size_t n) { return (n + 31) / 32; }
 constexpr uint32_t kDsumMinActors = 1u << 25;  // the summary is used from here (dbits > an L2)
 inline size_t dbits_alloc_words(size_t n) { return dbits_words(n) + (dbits_words(n) + 31) / 32; }
 // Full gossip on one GPU: the receipt tally (gp_kernels.h GsTally) is built from this many actors
-// and used in a round after one that emitted at least actors / kTallyThrDiv chains.
+// and used in a round after one that emitted at least actors / kTallyThrDiv chains (scaled by
+// the share of nodes not done).  With the batched placement 8 rather than 2: C4 66.7 -> 61.6 ms,
+// 10M +2% (profiles/round3/c4_scatter/cli_tally_thr.txt).
 constexpr size_t kTallyMinActors = 1u << 20;
 #ifndef GP_TALLY_THR_DIV
-#define GP_TALLY_THR_DIV 2
+#define GP_TALLY_THR_DIV 8
 #endif
 constexpr size_t kTallyThrDiv = GP_TALLY_THR_DIV;
 
