@@ -170,7 +170,7 @@ def gpu_same_window(eng, rounds, reps=3):
     return eng.actors * rounds / best
 
 
-def roofline(ks, bytes_per_update, actors, wl):
+def roofline(ks, bytes_per_update, actors, wl, rounds=None):
     """Round roofline: SURVEY §8(d) bytes per node-update x the node-updates one launch performs
     over the measured duration of one round = the round kernel + the pass that completes it (link
     scatter), both timed with hipEvents on the engine's stream inside the timed steps.  The
@@ -195,6 +195,9 @@ def roofline(ks, bytes_per_update, actors, wl):
             "avg_aux_ms": round(ks["aux_avg_ms"], 5), "round_ms": round(round_ms, 5),
             "bytes_per_launch": algo_bytes, "bytes_per_update": bytes_per_update,
             "updates_per_launch": round(units, 1), "actors": actors, "launches": ks["launches"],
+            # the launches the hipEvent brackets cover vs the rounds the timed steps ran: one GPU
+            # times every round (64-round groups); a shard samples every 8th round
+            "timed_launches": ks["launches"], "rounds": rounds,
             "frac_all_actors": round(bytes_per_update * actors / (round_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "layout_bytes_per_launch": ks["bytes_per_launch"],
             "layout_frac": round(ks["bytes_per_launch"] / (ks["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
@@ -245,8 +248,8 @@ def fail(msg):
     raise SystemExit(2)
 
 
-def roofline_for(ks, topology, algorithm, actors, wl):
-    return roofline(ks, survey_bytes_per_update(topology, algorithm), actors, wl)
+def roofline_for(ks, topology, algorithm, actors, wl, rounds=None):
+    return roofline(ks, survey_bytes_per_update(topology, algorithm), actors, wl, rounds)
 
 
 def base_line(args, rank, n_arg, topology, algorithm, window, devices):
@@ -289,7 +292,7 @@ def emit_line(args, *, name, n_arg, topology, algorithm, window, eng_actors, eng
                    "rounds_per_step": rounds_total / max(1, args.steps), "converged": converged,
                    "parallelism": parallelism},
         "wall_time_to_convergence_ms": elapsed * 1e3 / args.steps if not window else None,
-        "roofline": roofline_for(ks, topology, algorithm, own, wl),
+        "roofline": roofline_for(ks, topology, algorithm, own, wl, rounds_total),
         "cpu_baseline": cpu,
     }
     if extra:

@@ -407,8 +407,14 @@ int ensure_trace(Handle* h, int64_t need) {
     return GP_OK;
 }
 
-// Quiet-wave marks: one byte per segment of kActSeg actors.
-size_t act_bytes(const Handle* h) { return (size_t)(h->g.actors + kActSeg - 1u) / kActSeg + 1u; }
+// Quiet-wave marks: one byte per segment of kActSeg actors, indexed by global segment (actor >>
+// kActShift); a handle holds the segments of its actors [lo, hi) (+1 byte of padding).
+size_t act_first(const Handle* h) { return (size_t)(h->lo >> kActShift); }
+size_t act_bytes(const Handle* h) { return (size_t)((h->hi + kActSeg - 1u) >> kActShift) - act_first(h) + 1u; }
+int clear_act(Handle* h, int i) {
+    HIP_TRY(hipMemsetAsync(h->act[i] + act_first(h), 0, act_bytes(h), h->stream));
+    return GP_OK;
+}
 
 int reset(Handle* h) {
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -435,8 +441,10 @@ int reset(Handle* h) {
         } else {
             launch_fill_u8(h->dir[0] + xlo, kDirNone, xn, h->stream);
             launch_fill_u8(h->dir[1] + xlo, kDirNone, xn, h->stream);
-            for (uint8_t* q : h->act)
-                if (q) HIP_TRY(hipMemsetAsync(q, 0, act_bytes(h), h->stream));
+            for (int i = 0; i < 2; ++i) {
+                int rc;
+                if (h->act[i] && (rc = clear_act(h, i))) return rc;
+            }
         }
     } else {
         HIP_TRY(hipMemsetAsync(h->cnt + lo, 0, n * sizeof(uint32_t), h->stream));
@@ -484,7 +492,9 @@ bool full_quad(const Handle* h) { return h->gossip && h->full && !h->sharded && 
 bool fused_marks(const Handle* h) { return kFuseLinkMarks && !h->gossip && !h->generic && !h->sharded && h->g.has_link; }
 
 const char* round_kernel_name(const Handle* h) {
-    if (full_quad(h)) return "k_gs_full4";
+    // with the receipt tally the timed bracket also holds its passes (the scans, the placement and
+    // the per-bucket count, gp_kernels.hip launch_gs_tally), which run after k_gs_full4 every round
+    if (full_quad(h)) return h->tally.cnt ? "k_gs_full4+tally" : "k_gs_full4";
     if (h->gossip && !h->generic) {
         const bool e = gs_pull_early(h->args(0));
         return h->g.has_link ? (e ? "k_gs_pull<true, true>" : "k_gs_pull<true, false>")
@@ -492,7 +502,7 @@ const char* round_kernel_name(const Handle* h) {
     }
     if (h->gossip) return "k_gs_push";
     if (h->generic) return "k_ps_push_emit";
-    if (h->sharded && h->g.has_link) return h->rmsg[0] ? "k_ps_pull<2, false>" : "k_ps_pull<1, false>";
+    if (h->sharded && h->g.has_link && h->rmsg[0]) return h->act[0] ? "k_ps_quiet<2>" : "k_ps_pull<2, false>";
     if (h->g.has_link) return h->act[0] ? "k_ps_quiet<1>" : "k_ps_pull<1, false>";
     return h->act[0] ? "k_ps_quiet<0>" : "k_ps_pull<0, false>";
 }
@@ -538,9 +548,12 @@ int clear_tags_if_due(Handle* h, uint32_t r) {
     return GP_OK;
 }
 
-// The dominant round kernel F(k) (timed under GP_FLAG_KERNEL_TIMING) ...
-void launch_main(Handle* h, int64_t k, const Xchg* x) {
-    const RoundArgs a = h->args((uint32_t)k);
+// The dominant round kernel F(k) (timed under GP_FLAG_KERNEL_TIMING) ...  A shard samples the
+// timing of every kTimeEvery-th round (`timed`), and counts the actors its quiet kernel walks in
+// exactly those rounds, so work_per_launch and avg_ms average over the same launches.
+void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed) {
+    RoundArgs a = h->args((uint32_t)k);
+    if (h->sharded && !timed) a.work = nullptr;
     const Launch l = h->L();
     if (h->gossip) {
         if (h->generic) {  // adds into inc_cur, consumed (zeroed) by F(k+1)
@@ -606,8 +619,7 @@ int ensure_events(Handle* h, int64_t rounds) {
 // clear that array before a tag value repeats in it (after F(k - 1) has read it).
 int clear_act_if_due(Handle* h, int64_t k) {
     if (!h->act[0] || !tag_clear_round((uint32_t)(k + 1))) return GP_OK;
-    HIP_TRY(hipMemsetAsync(h->act[(k + 1) & 1], 0, act_bytes(h), h->stream));
-    return GP_OK;
+    return clear_act(h, (int)((k + 1) & 1));
 }
 
 // Round k with its three timing events (slot i of the event ring).
@@ -616,7 +628,7 @@ int launch_round(Handle* h, int64_t k, const Xchg* x, bool timing, int64_t i) {
     if (fused_marks(h) && (rc = clear_tags_if_due(h, (uint32_t)k))) return rc;
     if ((rc = clear_act_if_due(h, k))) return rc;
     if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i], h->stream));
-    launch_main(h, k, x);
+    launch_main(h, k, x, timing);
     if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i + 1], h->stream));
     if ((rc = launch_aux(h, k, x))) return rc;
     if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i + 2], h->stream));
@@ -712,14 +724,18 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         }
         h->completed = (int64_t)h->h_trace[real - 1];
         h->rounds += real;
-        if (group) {  // groups wholly inside the real rounds
+        if (group) {
+            // every group that holds a real round, launches = its real rounds, so the timed launches
+            // are exactly the run's rounds (the walked-actor count covers the same launches); the
+            // group that reaches convergence also times the gated no-op launches after it (a few us
+            // each: conservative)
             for (int64_t j = 0; j < ng; ++j) {
                 const int64_t first = j * every, last = std::min<int64_t>(first + every, B) - 1;
-                if (last >= real) break;
+                if (first >= real) break;
                 float ms = 0.f;
                 HIP_TRY(hipEventElapsedTime(&ms, h->kev[3 * j], h->kev[3 * j + 1]));
                 h->k_total_ms += ms;
-                h->k_launches += last - first + 1;
+                h->k_launches += std::min<int64_t>(last, real - 1) - first + 1;
             }
         } else if (timing && (rc = accumulate_timing(h, (real + kTimeEvery - 1) / kTimeEvery))) {
             return rc;
@@ -978,7 +994,7 @@ int shard_sync(Handle* h, gp_status* st) {
     if (of & 2u) return fail(GP_EOVERFLOW, "a shard received an entry outside its range; the run is void");
     if (of) return fail(GP_EOVERFLOW, "a shard exchange buffer overflowed; the run is void");
     const int64_t applied = (int64_t)applied_round(h, h->next_kernel - 1) + 1;  // rounds whose counts exist
-    int64_t timed_real = h->timed_count;
+    int64_t timed_real = h->converged ? 0 : h->timed_count;  // after convergence no round is real
     if (!h->converged && applied > h->rounds) {
         const int64_t n = applied - h->rounds;
         std::vector<unsigned long long> t((size_t)n);
@@ -997,6 +1013,7 @@ int shard_sync(Handle* h, gp_status* st) {
     }
     int rc;
     if (h->timed_count && (rc = accumulate_timing(h, timed_real))) return rc;
+    if (h->timed_count) h->work_rounds += timed_real;  // the quiet kernel counts in timed rounds only
     h->timed_count = 0;
     if (st) {
         std::memset(st, 0, sizeof *st);
@@ -1116,8 +1133,10 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
             if ((rc = h->alloc(&h->inc[0], n, lo)) || (rc = h->alloc(&h->inc[1], n, lo))) return bail(rc);
             if (full_quad(h) && (rc = h->alloc(&h->dbits, dbits_alloc_words(n)))) return bail(rc);
             const uint32_t nb = (uint32_t)((n + (1u << kTallyShift) - 1) >> kTallyShift);
+            // the tally is a speed path: where its 128 KB of dynamic LDS cannot be allowed (another
+            // ARCH), the handle keeps the receipt atomics, which give the same results
             if (full_quad(h) && nb <= kMaxTallyBuckets &&
-                (n >= kTallyMinActors || (cfg->flags & GP_FLAG_GOSSIP_TALLY))) {
+                (n >= kTallyMinActors || (cfg->flags & GP_FLAG_GOSSIP_TALLY)) && prepare_gs_tally() == 0) {
                 GsTally& t = h->tally;
                 t.nb = nb;
                 t.W = (uint32_t)h->grid;
@@ -1127,7 +1146,6 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
                     (rc = h->alloc(&t.scratch, scan_scratch_words((uint32_t)nc))) ||
                     (rc = h->alloc(&t.chains, (size_t)kPartRing * kParts * kPartStride)) || (rc = h->alloc(&t.on, 4)))
                     return bail(rc);
-                if (prepare_gs_tally()) return bail(fail(GP_EHIP, "hipFuncSetAttribute (tally LDS) failed"));
             }
         } else if ((rc = h->alloc(&h->dir[0], xn, xlo)) || (rc = h->alloc(&h->dir[1], xn, xlo))) {
             return bail(rc);
@@ -1139,10 +1157,10 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
             (rc = h->alloc(&h->flags, n, lo)) || (rc = h->alloc(&h->frozen, n, lo)) ||
             (rc = h->alloc(&h->partials, (size_t)h->grid)))
             return bail(rc);
-        if (GP_ACT_PCT > 0 && !h->generic && !h->sharded &&
-            (h->g.actors >= kQuietMinActors || (cfg->flags & GP_FLAG_QUIET_WAVES))) {  // quiet-wave marks
+        // quiet-wave marks (a shard: over its own actors; remote messages are marked by the unpack)
+        if (GP_ACT_PCT > 0 && !h->generic && (h->own() >= kQuietMinActors || (cfg->flags & GP_FLAG_QUIET_WAVES))) {
             for (int i = 0; i < 2; ++i)
-                if ((rc = h->alloc(&h->act[i], act_bytes(h)))) return bail(rc);
+                if ((rc = h->alloc(&h->act[i], act_bytes(h), (int64_t)act_first(h)))) return bail(rc);
             if ((rc = h->alloc(&h->work, (size_t)kParts * kWorkStride))) return bail(rc);
             if (hipMemsetAsync(h->work, 0, (size_t)kParts * kWorkStride * sizeof *h->work, h->stream) != hipSuccess)
                 return bail(fail(GP_EHIP, "hipMemsetAsync failed"));
@@ -1201,25 +1219,40 @@ struct Rccl {
     decltype(&ncclSend) send = nullptr;
     decltype(&ncclRecv) recv = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    std::string why;  // the loader's error text when a symbol or the library is missing
 };
 
-const Rccl* rccl() {
-    static Rccl r;
-    static bool tried = false;
-    if (!tried) {
-        tried = true;
+// Loaded once per process by a function-local static (thread-safe initialisation); the dlerror()
+// text is saved at load time, since a later dlerror() returns NULL or another call's message.
+const Rccl& rccl_state() {
+    static const Rccl r = [] {
+        Rccl x;
         void* so = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
         if (!so) so = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
-        if (so) {
-            r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(dlsym(so, "ncclCommInitAll"));
-            r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(so, "ncclCommDestroy"));
-            r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(so, "ncclGroupStart"));
-            r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(so, "ncclGroupEnd"));
-            r.send = reinterpret_cast<decltype(r.send)>(dlsym(so, "ncclSend"));
-            r.recv = reinterpret_cast<decltype(r.recv)>(dlsym(so, "ncclRecv"));
-            r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(so, "ncclGetErrorString"));
+        if (!so) {
+            const char* e = dlerror();
+            x.why = e ? e : "dlopen failed";
+            return x;
         }
-    }
+        auto sym = [&](const char* name) {
+            void* p = dlsym(so, name);
+            if (!p && x.why.empty()) x.why = std::string("missing symbol ") + name;
+            return p;
+        };
+        x.comm_init_all = reinterpret_cast<decltype(x.comm_init_all)>(sym("ncclCommInitAll"));
+        x.comm_destroy = reinterpret_cast<decltype(x.comm_destroy)>(sym("ncclCommDestroy"));
+        x.group_start = reinterpret_cast<decltype(x.group_start)>(sym("ncclGroupStart"));
+        x.group_end = reinterpret_cast<decltype(x.group_end)>(sym("ncclGroupEnd"));
+        x.send = reinterpret_cast<decltype(x.send)>(sym("ncclSend"));
+        x.recv = reinterpret_cast<decltype(x.recv)>(sym("ncclRecv"));
+        x.error_string = reinterpret_cast<decltype(x.error_string)>(sym("ncclGetErrorString"));
+        return x;
+    }();
+    return r;
+}
+
+const Rccl* rccl() {
+    const Rccl& r = rccl_state();
     const bool ok = r.comm_init_all && r.comm_destroy && r.group_start && r.group_end && r.send && r.recv &&
                     r.error_string;
     return ok ? &r : nullptr;
@@ -1404,7 +1437,8 @@ int group_create(const gp_config* cfg, gp_layout* out, void** handle) {
         hipError_t e = hipStreamCreateWithFlags(&G.shared, hipStreamNonBlocking);
         if (e != hipSuccess) return bail(fail(GP_EHIP, "hipStreamCreate: %s", hipGetErrorString(e)));
     } else if (!rccl()) {
-        return bail(fail(GP_ERCCL, "num_gpus %d needs RCCL: librccl.so.1 could not be loaded (%s)", W, dlerror()));
+        return bail(fail(GP_ERCCL, "num_gpus %d needs RCCL: librccl.so.1 could not be loaded (%s)", W,
+                         rccl_state().why.c_str()));
     }
     G.shard.assign((size_t)W, nullptr);
     G.send.assign((size_t)W, nullptr);

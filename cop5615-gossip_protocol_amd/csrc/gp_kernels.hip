@@ -418,7 +418,9 @@ __device__ __forceinline__ PsLevel1 ps_level1(const RoundArgs& a, const Geom& g,
     return p;
 }
 
-template <int LM, bool PRE = false>
+// FF: message loads for the first kFiredLoads FIRED link slots only (one GPU; the shards' quiet
+// kernel, which spills with one load per unrolled slot) instead of one per unrolled slot.
+template <int LM, bool PRE = false, bool FF = (LM == 1 || kFiredShards)>
 __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
                                               const PsLevel1& p, bool mark) {
     const uint32_t m = p.m;
@@ -529,7 +531,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
 #pragma unroll
             for (uint32_t k = 0; k < kLinkUnroll; ++k)
                 lk[k] = k < nl && ((kAblate & 131072u) ? ls[k] % 7u == 0u : lc[k] == a.tag_prev);  // round tags
-            if constexpr (LM != 0 && kFiredLoads < kLinkUnroll && (LM == 1 || kFiredShards)) {
+            if constexpr (LM != 0 && kFiredLoads < kLinkUnroll && FF) {
                 // load the messages of the first kFiredLoads FIRED slots only (about one slot in
                 // seven fires: 0.14 messages per actor), the rest on demand (rare).  A shard reads
                 // a remote source's message from the receiver's slot (rmsg_prev), a local one from
@@ -620,17 +622,20 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
     if (mark) {  // the waves with work in round r + 1: v's own if it still updates, its target's
         const uint8_t t = (uint8_t)link_tag(r + 1u);
         if (!(f & 16u)) byte_store<GP_ACT_POL>(&a.act_cur[v >> kActShift], t);
-        if (o.send)
-            byte_store<GP_ACT_POL>(
-                &a.act_cur[dir_target(g, v, code, code == kDirLink ? link_of(a.seed, v, a.nodes) : 0u) >> kActShift], t);
+        if (o.send) {
+            const uint32_t tv = dir_target(g, v, code, code == kDirLink ? link_of(a.seed, v, a.nodes) : 0u);
+            // a shard marks its own actors only: the receiver of a message that leaves the range
+            // marks it when the exchange delivers it (k_shard_unpack)
+            if (!a.sharded || tv - a.lo < a.hi - a.lo) byte_store<GP_ACT_POL>(&a.act_cur[tv >> kActShift], t);
+        }
     }
     return o.conv_now ? 1u : 0u;
 }
 
-template <int LM>
+template <int LM, bool FF = (LM == 1 || kFiredShards)>
 __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
                                              bool mark = false) {
-    return ps_finish<LM>(a, g, r, v, ps_level1<LM>(a, g, r, v), mark);
+    return ps_finish<LM, false, FF>(a, g, r, v, ps_level1<LM>(a, g, r, v), mark);
 }
 
 // The quiet-wave tail with compaction.  Marks are per segment of kActSeg actors: F(r) marks the
@@ -663,12 +668,14 @@ __device__ __forceinline__ uint32_t tail_mark(const RoundArgs& a, const TailWalk
 __device__ __forceinline__ TailWalk tail_walk(const RoundArgs& a, bool tail) {
     __shared__ uint32_t seg_list[kBlock / 64u * kTailList];
     TailWalk t;
-    const uint32_t nseg = (a.hi + kActSeg - 1u) >> kActShift;  // one GPU: actors [0, hi)
+    // segments are global (actor >> kActShift): a shard walks the ones that hold its actors
+    // [lo, hi); a segment astride lo or hi is walked by both ranks, each for its own actors
+    const uint32_t sg0 = a.lo >> kActShift, sg1 = (a.hi + kActSeg - 1u) >> kActShift, nseg = sg1 - sg0;
     const uint32_t grp = blockIdx.x & 7u, wpg = (gridDim.x >> 3) * (kBlock / 64u);
     const uint32_t wid = (blockIdx.x >> 3) * (kBlock / 64u) + (threadIdx.x >> 6);
     const uint32_t sspan = ((nseg + 7u) / 8u + 63u) / 64u * 64u;
-    const uint32_t s0 = grp * sspan;
-    t.s1 = s0 + sspan < nseg ? s0 + sspan : nseg;
+    const uint32_t s0 = sg0 + grp * sspan;
+    t.s1 = s0 + sspan < sg1 ? s0 + sspan : sg1;
     t.base = s0 + wid * 64u;
     t.stride = wpg * 64u;
     t.c = t.k = 0;
@@ -783,8 +790,8 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a) {
                 u = v;
                 v += step;
             }
-            if (u < a.hi) {
-                newly += ps_actor<LM>(a, g, r, u, mark);
+            if (u - a.lo < a.hi - a.lo) {  // lo <= u < hi (a shard's edge segments)
+                newly += ps_actor<LM, LM == 1 || LM == 2 || kFiredShards>(a, g, r, u, mark);
                 ++walked;
             }
         }
@@ -1209,6 +1216,12 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
         a.total[applied] = (applied >= 1 ? a.total[applied - 1] : 0ull) + t;
         if (of) atomicOr(x.overflow, 1u);
     }
+    // Quiet-tail marks (push-sum): when F(applied) marked the segments with work in
+    // the next round (the count after the round before it reached act_thr), the segment of every
+    // actor of this rank that a remote message reaches is marked here, with F(applied)'s tag.
+    const bool mark = !gossip && a.act_cur != nullptr && applied >= 0 &&
+                      (applied >= 1 ? a.total[applied - 1] : 0ull) >= (unsigned long long)a.act_thr;
+    const uint8_t mtag = (uint8_t)link_tag((uint32_t)applied + 1u);
     // halo faces: direction bytes of the neighbour's face plane, then its crossing messages
     const uint32_t gtid = blockIdx.x * kBlock + threadIdx.x, gstride = gridDim.x * kBlock;
     for (int side = 0; side < 2; ++side) {
@@ -1227,6 +1240,8 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
                 continue;
             }
             a.msg_cur[first + o] = x.h.in_msg[side][i];
+            // the message crosses the face toward this rank (code[side] is the outgoing one)
+            if (mark) a.act_cur[dir_target(a.g, first + o, x.h.code[side] ^ 1u, 0u) >> kActShift] = mtag;
         }
     }
     // an entry outside this rank's actors / slots can only come from a corrupt chunk: it is
@@ -1254,6 +1269,15 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
                 a.rmsg_cur[t] = in.msg[i];
                 a.lcnt_cur[t] = (uint8_t)a.tag_cur;  // plain: non-temporal marks and messages
                                                      // cost 0.29 ms more per round (C5 / 8)
+                if (mark) {  // the receiver owning slot t: the last v in [lo, hi) with rev_off[v] <= t
+                    uint32_t l = a.lo, h = a.hi;
+                    while (h - l > 1u) {
+                        const uint32_t mid = l + ((h - l) >> 1);
+                        if (a.rev_off[mid] <= t) l = mid;
+                        else h = mid;
+                    }
+                    a.act_cur[l >> kActShift] = mtag;
+                }
             }
         }
     }
@@ -1987,8 +2011,9 @@ void launch_ps_pull(const RoundArgs& a, const Launch& l) {
     if (!a.g.has_link) {
         if (q) hipLaunchKernelGGL((k_ps_quiet<0>), dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a);
         else hipLaunchKernelGGL((k_ps_pull<0, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
-    } else if (a.rmsg_prev) {
-        hipLaunchKernelGGL((k_ps_pull<2, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
+    } else if (a.rmsg_prev) {  // a shard of several ranks
+        if (q) hipLaunchKernelGGL((k_ps_quiet<2>), dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a);
+        else hipLaunchKernelGGL((k_ps_pull<2, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
     } else if (q) {
         hipLaunchKernelGGL((k_ps_quiet<1>), dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a);
     } else {

@@ -39,7 +39,9 @@ class HipShard:
 
     def __init__(self, n_arg: int, topology: str, algorithm: str, *, rank: int, world: int, seed: int = 1,
                  device: int = 0, stream: int | None = None, kernel_timing: bool = False, delta: float = 1e-10,
-                 gossip_threshold: int = 10, term_init: int = 1, term_limit: int = 3):
+                 gossip_threshold: int = 10, term_init: int = 1, term_limit: int = 3, quiet_waves: bool = False):
+        """quiet_waves: the push-sum quiet-tail walk at any shard size (a test hook; on by default
+        for shards of 2^20 actors or more)."""
         import torch
 
         if topology not in _abi.TOPOLOGIES:
@@ -50,6 +52,7 @@ class HipShard:
         # torch's current stream by default, so the exchange (RCCL / copies) is ordered with the
         # kernels; its handle may be 0 (the null stream), hence FLAG_USE_STREAM
         flags = (_abi.FLAG_KERNEL_TIMING if kernel_timing else 0) | _abi.FLAG_USE_STREAM
+        flags |= _abi.FLAG_QUIET_WAVES if quiet_waves else 0
         if stream is None:
             stream = torch.cuda.current_stream(device).cuda_stream
         self.cfg = _abi.Config(n_arg, _abi.TOPOLOGIES[topology], _abi.ALGOS[algorithm], seed, delta,

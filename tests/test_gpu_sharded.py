@@ -123,6 +123,86 @@ def test_shards_vs_single_gpu_world8(n, topo, algo, rounds):
     _check_vs(ref, engines, algo)
 
 
+# The quiet-tail walk on shards: once 99% of the nodes have converged, a rank
+# walks only the 4-actor segments marked by its own round kernel (its own actors still updating,
+# the targets of its own local messages) and by its unpack (the targets of the halo and link
+# messages other ranks sent it).  Forced at small sizes, run to convergence, bit-exact against the
+# oracle; the C3 x8 fingerprint covers the default size gate (2^20 actors per rank).
+QUIET_SHARD_CASES = [
+    (1000, "Imp3D", 2, 1), (20000, "Imp3D", 3, 5), (200000, "Imp3D", 4, 3), (300000, "Imp3D", 8, 11),
+    (8000, "3D", 3, 2), (2000, "line", 3, 4), (3000, "2D", 2, 6), (64000, "3D", 5, 8),
+]
+
+
+@pytest.mark.parametrize("n,topo,world,seed", QUIET_SHARD_CASES)
+def test_shards_quiet_tail_vs_oracle(n, topo, world, seed):
+    ref = oracle.OracleSim(n, topo, "push-sum", seed=seed)
+    rs = ref.step(1 << 20, threads=8)
+    engines = _shards(n, topo, "push-sum", world, seed, quiet_waves=True)
+    sts = sharded.run_local(engines, max_rounds=1 << 20)
+    assert rs.converged
+    for st in sts:
+        assert (st.round, st.completed, st.converged) == (rs.round, rs.completed, rs.converged)
+    _check_vs(ref, engines, "push-sum")
+    # a second run after a reset: no mark of the first run may leak into it
+    for e in engines:
+        e.reset()
+    sts = sharded.run_local(engines, max_rounds=1 << 20)
+    assert (sts[0].round, sts[0].completed) == (rs.round, rs.completed)
+    _check_vs(ref, engines, "push-sum")
+    for e in engines:
+        e.close()
+
+
+def _quiet_shard_sweep(count=16, seed=99):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(count):
+        topo = ("Imp3D", "3D", "line", "2D", "Imp3D")[rng.integers(5)]
+        hi = 3000 if topo in ("line", "2D") else 150000
+        out.append((int(np.exp(rng.uniform(np.log(64), np.log(hi)))), topo, int(rng.integers(2, 9)),
+                    int(rng.integers(1, 1 << 30))))
+    return out
+
+
+@pytest.mark.parametrize("n,topo,world,seed", _quiet_shard_sweep())
+def test_shards_quiet_tail_random_sweep(n, topo, world, seed):
+    try:
+        sharded.partition(n, topo, world)
+    except GossipError as e:
+        if "cannot be split" not in str(e):
+            raise
+        pytest.skip(str(e))
+    ref = oracle.OracleSim(n, topo, "push-sum", seed=seed)
+    rs = ref.step(1 << 20, threads=8)
+    engines = _shards(n, topo, "push-sum", world, seed, quiet_waves=True)
+    sts = sharded.run_local(engines, max_rounds=int(rs.round))
+    for st in sts:
+        assert (st.round, st.completed, st.converged) == (rs.round, rs.completed, rs.converged)
+    _check_vs(ref, engines, "push-sum")
+    for e in engines:
+        e.close()
+
+
+def test_shards_quiet_default_and_work_count():
+    """Shards of 2^20 actors or more run the quiet kernel by default (k_ps_quiet<2>), and count the
+    actors it walks in their timed rounds only, so work_per_launch averages over the same launches
+    as the kernel time: below the shard's actor count (the tail walks a few per cent of it)."""
+    n, world = 4_500_000, 2
+    ref = Simulator(n, "Imp3D", "push-sum", seed=3)
+    rs = ref.step()
+    engines = _shards(n, "Imp3D", "push-sum", world, seed=3, kernel_timing=True)
+    sts = sharded.run_local(engines)
+    assert (sts[0].round, sts[0].completed, sts[0].converged) == (rs.round, rs.completed, rs.converged)
+    _check_vs(ref, engines, "push-sum")
+    for e in engines:
+        ks = e.kernel_stats()
+        assert ks["kernel"] == "k_ps_quiet<2>", ks
+        assert ks["launches"] == (int(rs.round) + 7) // 8, ks  # every 8th round is timed
+        assert 0 < ks["work_per_launch"] < e.hi - e.lo, ks
+        e.close()
+
+
 def test_shards_imp3d_10m_two_ranks():
     """BASELINE config 3 split over 2 shards: the same run as the single-GPU engine."""
     ref = Simulator(10_000_000, "Imp3D", "push-sum", seed=1)

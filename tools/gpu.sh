@@ -15,6 +15,8 @@
 #   ktrun_bench  kernel trace of bench.py with the arguments given as the second argument
 #   pmcrun  FETCH_SIZE and WRITE_SIZE passes over a whole run (prof_run.py, $ROUNDS default: to
 #           convergence) -> tools/pmc_run_summary.py ($PMC_WORKLOAD, $PMC_KERNEL) into $O
+#   pmcgroup the same passes, summed over the kernels of one round ($PMC_KERNELS, comma list) and
+#           divided by $PMC_ROUNDS -> tools/pmc_group_summary.py ($PMC_WORKLOAD, $PMC_GROUP)
 # Extra prof_run.py arguments: $PROF_ARGS; rounds: $ROUNDS; bench.py arguments: $BENCH_ARGS;
 # output directory name: $OUT (default: the mode).
 set -o pipefail
@@ -69,6 +71,12 @@ case $MODE in
       rc=$?; echo "pmc $c rc=$rc"; tail -1 "$O/pmc_$c.log"; [ $rc -eq 0 ] || exit $rc
     done
     python3 "$R/tools/pmc_run_summary.py" "$O/pmc_FETCH_SIZE" "$O/pmc_WRITE_SIZE" "$O/pmc_run.json" "${PMC_WORKLOAD:-10000000 Imp3D push-sum}" "${PMC_KERNEL:-k_ps_quiet<1>}" ;;
+  pmcgroup)
+    for c in FETCH_SIZE WRITE_SIZE; do
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_$c" -o p -- python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-1000000} ${PROF_ARGS} > "$O/pmc_$c.log" 2>&1 )
+      rc=$?; echo "pmc $c rc=$rc"; tail -1 "$O/pmc_$c.log"; [ $rc -eq 0 ] || exit $rc
+    done
+    python3 "$R/tools/pmc_group_summary.py" "$O/pmc_FETCH_SIZE" "$O/pmc_WRITE_SIZE" "$O/pmc_group.json" "$PMC_WORKLOAD" "$PMC_GROUP" "$PMC_ROUNDS" "$PMC_KERNELS" ;;
   cli)
     IFS=';' read -ra CASES <<< "${CLI_CASES:-10000000 Imp3D push-sum}"
     for c in "${CASES[@]}"; do

@@ -1,10 +1,19 @@
 """W shards of one graph on ONE GPU (loopback exchange): per-kernel cost of the shard round at a
-realistic remote fraction (e.g. 8 ranks -> 7/8 of the extra links remote), for A/B builds.
+realistic remote fraction (e.g. 8 ranks -> 7/8 of the extra links remote), for A/B builds, and the
+per-round cost of a whole run (every rank's round + the chunk copies + every rank's unpack,
+bracketed with hipEvents on the shards' stream) with the phases of the run marked.
 
     python3 tools/shard_loopback_prof.py --world 8 --n 80000000 --rounds 64
+    python3 tools/shard_loopback_prof.py --world 8 --n 100000000 --series out.json   # to convergence
+
+The ranks run one after another on one GPU, so a round's time / world is the cost of one
+rank-round without RCCL.  The summary compares the rounds in which every actor still sends (before
+the first convergence) with the rounds after 99% of the nodes have converged (the quiet tail).
 """
 import argparse
+import json
 import os
+import statistics
 import sys
 import time
 
@@ -16,7 +25,9 @@ ap.add_argument("--n", type=int, default=80_000_000)
 ap.add_argument("--world", type=int, default=8)
 ap.add_argument("--topology", default="Imp3D")
 ap.add_argument("--algorithm", default="push-sum")
-ap.add_argument("--rounds", type=int, default=64)
+ap.add_argument("--rounds", type=int, default=None, help="default: to convergence")
+ap.add_argument("--seed", type=int, default=1)
+ap.add_argument("--series", default=None, help="write the per-round series (JSON) here")
 a = ap.parse_args()
 
 import torch  # noqa: E402
@@ -24,17 +35,69 @@ import torch  # noqa: E402
 from gossip_amd import sharded  # noqa: E402
 
 torch.cuda.set_device(0)
-shards = [sharded.HipShard(a.n, a.topology, a.algorithm, rank=r, world=a.world, seed=1, kernel_timing=True)
+shards = [sharded.HipShard(a.n, a.topology, a.algorithm, rank=r, world=a.world, seed=a.seed, kernel_timing=True)
           for r in range(a.world)]
-sharded.run_local(shards, max_rounds=8)
+nodes = shards[0].nodes
+sharded.run_local(shards, max_rounds=8)  # warm-up (module load, first touches)
+for e in shards:
+    e.reset()
+    e.kernel_stats(reset=True)
 torch.cuda.synchronize()
+cap = a.rounds if a.rounds else 1 << 40
+t = sharded.LoopbackTransport()
+events = []
+sts = [e.sync() for e in shards]
+batch = 8
 t0 = time.perf_counter()
-sts = sharded.run_local(shards, max_rounds=a.rounds)
+while not sts[0].converged and sts[0].round < cap:
+    for _ in range(min(batch, cap - int(sts[0].round))):
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        for e in shards:
+            e.round()
+        t.exchange_all(shards)
+        for e in shards:
+            e.deliver()
+        ev[1].record()
+        events.append(ev)
+    sts = [e.sync() for e in shards]
+    assert len({(int(s.round), int(s.completed), int(s.converged)) for s in sts}) == 1, "shards disagree"
+    batch = min(batch * 2, 64)
 torch.cuda.synchronize()
 el = time.perf_counter() - t0
+rounds = int(sts[0].round)
+trace = [int(x) for x in shards[0].read_trace()]
+# gossip's F(k) applies round k - 1: one launch more than rounds
+launches = rounds + (1 if a.algorithm == "gossip" else 0)
+per_round = [events[i][0].elapsed_time(events[i][1]) for i in range(min(launches, len(events)))]
 ks = shards[0].kernel_stats()
-print(f"{a.world} shards of {a.n} {a.topology} {a.algorithm}: {a.rounds} rounds in {el * 1e3:.1f} ms "
-      f"(all shards serialised on one GPU); rank 0 {ks['kernel']} {ks['avg_ms'] * 1e3:.1f} us, "
-      f"{ks['aux_kernel']} {ks['aux_avg_ms'] * 1e3:.1f} us", flush=True)
+
+
+def mean(xs):
+    return statistics.fmean(xs) if xs else None
+
+
+# round r is "all-sending" while no node had converged after round r - 1; "tail" once 99% had
+prev = [0] + trace[:-1]
+dense = [per_round[r] for r in range(len(per_round)) if r < len(prev) and prev[r] == 0]
+tail = [per_round[r] for r in range(len(per_round)) if r < len(prev) and prev[r] * 100 >= 99 * nodes]
+summary = {
+    "workload": f"{a.n} {a.topology} {a.algorithm}", "world": a.world, "rounds": rounds,
+    "converged": bool(sts[0].converged), "host_ms": el * 1e3,
+    "round_ms_sum": sum(per_round),
+    "rank_round_ms_all_sending": mean(dense) / a.world if dense else None,
+    "rank_round_ms_tail_99": mean(tail) / a.world if tail else None,
+    "tail_over_all_sending": (mean(tail) / mean(dense)) if dense and tail else None,
+    "rounds_all_sending": len(dense), "rounds_tail_99": len(tail),
+    "rank0_kernel": ks["kernel"], "rank0_kernel_avg_ms": ks["avg_ms"], "rank0_aux": ks["aux_kernel"],
+    "rank0_aux_avg_ms": ks["aux_avg_ms"], "rank0_work_per_launch": ks["work_per_launch"],
+    "rank0_actors": shards[0].hi - shards[0].lo,
+    "bytes_sent_per_round_rank0": sum(shards[0].send_splits),
+    "note": "all ranks serialised on one GPU; exchange = device copies (no RCCL); rank-round = round / world",
+}
+print(json.dumps(summary, indent=1), flush=True)
+if a.series:
+    with open(a.series, "w") as f:
+        json.dump(dict(summary, per_round_ms=[round(x, 4) for x in per_round], trace=trace), f)
 for e in shards:
     e.close()
