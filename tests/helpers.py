@@ -3,6 +3,10 @@ import base64
 import hashlib
 import json
 import os
+import socket
+import subprocess
+import sys
+import tempfile
 import zlib
 
 import numpy as np
@@ -115,3 +119,31 @@ def check_same(a, b, algo):
         np.testing.assert_array_equal(bits(sa), bits(sb))
         np.testing.assert_array_equal(bits(wa), bits(wb))
     np.testing.assert_array_equal(a.read_trace(), b.read_trace())
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_dist_job(world, backend, n, topology, algorithm, seed, cap, timeout):
+    """Launch tests/dist_shard_job.py under torch.distributed.run with `world` ranks; returns the
+    rank parts (status, trace, state arrays) in rank order."""
+    out = tempfile.mkdtemp(prefix="gp_dist_")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_shard_job.py"), "--backend", backend, "--n-arg", str(n),
+           "--topology", topology, "--algorithm", algorithm, "--seed", str(seed), "--cap", str(cap), "--out", out]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
+    parts = []
+    for q in range(world):
+        with np.load(os.path.join(out, f"rank{q}.npz"), allow_pickle=False) as z:
+            parts.append({k: z[k] for k in z.files})
+    return parts
+
+
+def join_parts(parts, keys):
+    return {k: np.concatenate([p[k] for p in parts]) for k in keys}

@@ -170,3 +170,26 @@ def test_sharded_random_sweep(case, world):
             raise
         pytest.skip(str(e))
     test_sharded_matches_single_process(case, world)
+
+
+@pytest.mark.parametrize("world,case", [(2, (1000, "Imp3D", "push-sum", 1, 0)), (3, (1000, "full", "gossip", 2, 0))],
+                         ids=lambda c: str(c))
+def test_dist_shard_job_script_gloo(world, case):
+    """The launcher and rank script of the cross-device nccl test (tests/dist_shard_job.py under
+    torch.distributed.run, test_gpu_multidevice.py) on CPU: gloo + the oracle's shard engine, the
+    joined rank parts bit-exact against one process."""
+    import oracle
+    from helpers import join_parts, run_dist_job, state_arrays
+
+    n, topo, algo, seed, cap = case
+    ref = oracle.OracleSim(n, topo, algo, seed=seed)
+    rs = ref.step()
+    want = state_arrays(ref, algo)
+    parts = run_dist_job(world, "gloo", n, topo, algo, seed, cap, 300)
+    for p in parts:
+        assert tuple(int(x) for x in p["status"]) == (rs.round, rs.completed, rs.converged)
+        np.testing.assert_array_equal(p["trace"], ref.read_trace())
+    got = join_parts(parts, list(want))
+    for k in want:
+        np.testing.assert_array_equal(got[k], want[k])
+    ref.close()
