@@ -106,6 +106,23 @@ size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
 struct Group;
 
+// Restore point of a push-sum shard under activity tiers (gp_shard_sync): the state F(k0) reads
+// (the round k0-1 messages, direction bytes, link marks and remote link messages, the flags and
+// the quiet-tail marks of round k0) and the host's counters at that round.
+struct Ckpt {
+    bool valid = false;
+    int64_t next_kernel = 0, rounds = 0, completed = 0;
+    int64_t k_launches = 0, work_rounds = 0;
+    double k_total_ms = 0.0, k_aux_ms = 0.0;
+    double2* msg = nullptr;
+    uint8_t* dir = nullptr;
+    uint8_t* lcnt = nullptr;
+    double2* rmsg = nullptr;
+    uint8_t* flags = nullptr;
+    uint8_t* act = nullptr;
+    unsigned long long* work = nullptr;
+};
+
 struct Handle {
     Group* grp = nullptr;  // num_gpus > 1: this handle is the whole graph over the group's shards
     gp_config cfg{};
@@ -123,6 +140,14 @@ struct Handle {
     std::vector<int64_t> out_off, in_off;     // chunk offsets inside the send / recv buffers
     int64_t send_total = 0, recv_total = 0;
     uint32_t max_in_cap = 0;
+    std::vector<Chunk> full_out, full_in;  // the full plan (the buffers are sized for it)
+    uint32_t* pmax = nullptr;      // running max of link entries per sub-segment to each peer
+    const void* last_recv = nullptr;  // the receive buffer of the last gp_shard_deliver
+    Ckpt ck;                       // activity tiers: the restore point (push-sum shards)
+    int64_t full_until = 0;        // after a restore: the full plan until this many rounds are final
+    bool tiered = false;           // the batch in flight may run reduced chunks (a global decision)
+    int64_t delivered = 0;         // rounds delivered since the plan was last chosen
+    int64_t plan_changes = 0, restores = 0;
     uint32_t* pcount = nullptr;
     uint32_t* overflow = nullptr;
     unsigned long long* self_newly = nullptr;
@@ -416,6 +441,8 @@ int clear_act(Handle* h, int i) {
     return GP_OK;
 }
 
+void full_plan(Handle* h);
+
 int reset(Handle* h) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     const size_t lo = h->lo, n = h->own();
@@ -483,6 +510,16 @@ int reset(Handle* h) {
     h->batch = 8;
     h->awaiting_deliver = false;
     h->timed_count = 0;
+    if (h->sharded) {  // the full plan, no restore point
+        HIP_TRY(hipMemsetAsync(h->pmax, 0, kMaxWorld * sizeof(uint32_t), h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        h->ck.valid = false;
+        h->tiered = false;
+        h->delivered = 0;
+        h->full_until = 0;
+        h->last_recv = nullptr;
+        if (!h->full_out.empty()) full_plan(h);
+    }
     return GP_OK;
 }
 
@@ -844,18 +881,29 @@ Chunk chunk_layout(const Handle* h, int p, int q) {
     return c;
 }
 
-int build_plan(Handle* h) {
-    const int W = h->world, p = h->rank;
-    h->out_chunk.assign((size_t)W, Chunk{});
-    h->in_chunk.assign((size_t)W, Chunk{});
-    h->out_off.assign((size_t)W, 0);
-    h->in_off.assign((size_t)W, 0);
+// The chunk `full` with `cap` link entries per sub-segment (the header and halo part unchanged).
+Chunk with_cap(const Chunk& full, uint32_t cap) {
+    Chunk c = full;
+    c.cap = cap;
+    size_t off = align_up(c.slot + (size_t)kSub * cap * sizeof(uint32_t));
+    if (full.msg) {
+        c.msg = off;
+        off = align_up(off + (size_t)kSub * cap * sizeof(double2));
+    }
+    c.size = off;
+    return c;
+}
+
+// The current plan: chunk p -> q of every peer with the link capacities out_cap[q] / in_cap[q]
+// (the full plan's at most), packed from offset 0 of the send / receive buffers.
+void apply_plan(Handle* h, const std::vector<uint32_t>& out_cap, const std::vector<uint32_t>& in_cap) {
+    const int W = h->world;
     int64_t so = 0, ro = 0;
     h->max_in_cap = 0;
     for (int q = 0; q < W; ++q) {
-        if (q != p) {
-            h->out_chunk[q] = chunk_layout(h, p, q);
-            h->in_chunk[q] = chunk_layout(h, q, p);
+        if (q != h->rank) {
+            h->out_chunk[q] = with_cap(h->full_out[q], std::min(out_cap[q], h->full_out[q].cap));
+            h->in_chunk[q] = with_cap(h->full_in[q], std::min(in_cap[q], h->full_in[q].cap));
             h->max_in_cap = std::max(h->max_in_cap, h->in_chunk[q].cap);
         }
         h->out_off[q] = so;
@@ -863,10 +911,40 @@ int build_plan(Handle* h) {
         so += (int64_t)h->out_chunk[q].size;
         ro += (int64_t)h->in_chunk[q].size;
     }
-    h->send_total = so;
-    h->recv_total = ro;
+}
+
+void full_plan(Handle* h) {
+    std::vector<uint32_t> o((size_t)h->world), i((size_t)h->world);
+    for (int q = 0; q < h->world; ++q) {
+        o[q] = h->full_out[q].cap;
+        i[q] = h->full_in[q].cap;
+    }
+    apply_plan(h, o, i);
+}
+
+int build_plan(Handle* h) {
+    const int W = h->world, p = h->rank;
+    h->full_out.assign((size_t)W, Chunk{});
+    h->full_in.assign((size_t)W, Chunk{});
+    h->out_chunk.assign((size_t)W, Chunk{});
+    h->in_chunk.assign((size_t)W, Chunk{});
+    h->out_off.assign((size_t)W, 0);
+    h->in_off.assign((size_t)W, 0);
+    for (int q = 0; q < W; ++q)
+        if (q != p) {
+            h->full_out[q] = chunk_layout(h, p, q);
+            h->full_in[q] = chunk_layout(h, q, p);
+        }
+    full_plan(h);
+    h->send_total = 0;
+    h->recv_total = 0;
+    for (int q = 0; q < W; ++q) {
+        h->send_total += (int64_t)h->out_chunk[q].size;
+        h->recv_total += (int64_t)h->in_chunk[q].size;
+    }
     int rc;
-    if ((rc = h->alloc(&h->pcount, ((size_t)W + 2) * kSub * kCtrStride)) || (rc = h->alloc(&h->overflow, 1)) || (rc = h->alloc(&h->self_newly, 1)))
+    if ((rc = h->alloc(&h->pcount, ((size_t)W + 2) * kSub * kCtrStride)) || (rc = h->alloc(&h->overflow, 1)) ||
+        (rc = h->alloc(&h->self_newly, 1)) || (rc = h->alloc(&h->pmax, kMaxWorld)))
         return rc;
     return GP_OK;
 }
@@ -883,6 +961,7 @@ Xchg base_xchg(const Handle* h) {
     x.pcount = h->pcount;
     x.overflow = h->overflow;
     x.self_newly = h->self_newly;
+    x.pmax = h->pmax;
     return x;
 }
 
@@ -982,7 +1061,152 @@ int shard_deliver(Handle* h, const void* recv) {
                         h->gossip ? 1 : 0, h->full ? 1 : 0, h->stream);
     HIP_TRY(hipGetLastError());
     h->awaiting_deliver = false;
+    h->last_recv = recv;
+    ++h->delivered;
     h->next_kernel = k + 1;
+    return GP_OK;
+}
+
+// ---- activity tiers (push-sum shards of several ranks)
+// The link entries a rank sends per round follow the run's activity: every actor sends while it
+// updates, and in the converged tail only relayed messages move (a few per cent of the actors), yet
+// the full plan ships the capacity of an all-sending round (C5 / 8: ~0.31 GB per rank per round).
+// At every gp_shard_sync both ends of a chunk p -> q know the most entries one of its sub-segments
+// held in the batch just run (p from its own counters, q from p's last header), and size the next
+// batch's chunk from it: the full capacity halved while the half still holds twice that count plus
+// 64.  Counts can still outgrow a reduced chunk (overflow is detected, never silent), so a reduced
+// plan runs only after a restore point: the state the next round reads, copied at a sync every
+// kCkptEvery rounds.  A batch that overflowed is discarded on every rank (the overflow flag travels
+// in every header) and the ranks resume from the restore point with the full plan up to the round
+// the failed batch reached, so the run stays exact.  Every decision is made from values every rank
+// (or both ends of a chunk) holds, so the ranks agree without an extra exchange.
+constexpr int64_t kCkptEvery = 256;
+
+bool tiers_on(const Handle* h) {
+    return h->sharded && h->world > 1 && !h->gossip && !h->generic && !(h->cfg.flags & GP_FLAG_FULL_PLAN);
+}
+
+uint32_t tier_cap(uint32_t full, uint32_t m, bool tight) {
+    const uint64_t need = tight ? (uint64_t)m : 2ull * m + 64u;
+    uint32_t c = full;
+    while (c > 1u && (uint64_t)((c + 1u) / 2u) >= need && (c + 1u) / 2u < c) c = (c + 1u) / 2u;
+    return c;
+}
+
+int ensure_ckpt(Handle* h) {
+    Ckpt& c = h->ck;
+    if (c.msg) return GP_OK;
+    const size_t xn = (size_t)(h->ext_hi() - h->ext_lo()), n = h->own();
+    const size_t nsl = (size_t)(h->sbnd.empty() ? 0 : h->sbnd[h->rank + 1] - h->sbnd[h->rank]);
+    int rc;
+    if ((rc = h->alloc(&c.msg, xn)) || (rc = h->alloc(&c.dir, xn)) || (rc = h->alloc(&c.flags, n)) ||
+        (rc = h->alloc(&c.work, (size_t)kParts * kWorkStride)))
+        return rc;
+    if (h->lcnt[0] && ((rc = h->alloc(&c.lcnt, nsl)) || (rc = h->alloc(&c.rmsg, nsl)))) return rc;
+    if (h->act[0] && (rc = h->alloc(&c.act, act_bytes(h)))) return rc;
+    return GP_OK;
+}
+
+// Copy the state F(k0) reads (k0 = next_kernel) into (save) or out of (!save) the restore point.
+int ckpt_copy(Handle* h, bool save) {
+    Ckpt& c = h->ck;
+    const int64_t k0 = h->next_kernel;
+    const int p = (int)((k0 + 1) & 1);  // parity of round k0 - 1
+    const size_t xlo = (size_t)h->ext_lo(), xn = (size_t)(h->ext_hi() - h->ext_lo()), lo = h->lo, n = h->own();
+    hipStream_t s = h->stream;
+    auto cp = [&](void* live, void* saved, size_t bytes) {
+        return save ? hipMemcpyAsync(saved, live, bytes, hipMemcpyDeviceToDevice, s)
+                    : hipMemcpyAsync(live, saved, bytes, hipMemcpyDeviceToDevice, s);
+    };
+    HIP_TRY(cp(h->msg[p] + xlo, c.msg, xn * sizeof(double2)));
+    HIP_TRY(cp(h->dir[p] + xlo, c.dir, xn));
+    HIP_TRY(cp(h->flags + lo, c.flags, n));
+    HIP_TRY(cp(h->work, c.work, (size_t)kParts * kWorkStride * sizeof *h->work));
+    if (h->lcnt[0]) {
+        const size_t slo = (size_t)h->sbnd[h->rank], nsl = (size_t)(h->sbnd[h->rank + 1] - h->sbnd[h->rank]);
+        HIP_TRY(cp(h->lcnt[p] + slo, c.lcnt, nsl));
+        HIP_TRY(cp(h->rmsg[p] + slo, c.rmsg, nsl * sizeof(double2)));
+        // the marks of round k0 land in the other array: a failed batch's are cleared
+        if (!save) HIP_TRY(hipMemsetAsync(h->lcnt[p ^ 1] + slo, 0, nsl, s));
+    }
+    if (h->act[0]) HIP_TRY(cp(h->act[k0 & 1] + act_first(h), c.act, act_bytes(h)));
+    if (save) {
+        c.next_kernel = k0;
+        c.rounds = h->rounds;
+        c.completed = h->completed;
+        c.k_launches = h->k_launches;
+        c.k_total_ms = h->k_total_ms;
+        c.k_aux_ms = h->k_aux_ms;
+        c.work_rounds = h->work_rounds;
+        c.valid = true;
+    }
+    return GP_OK;
+}
+
+// Back to the restore point after an overflowed batch (every rank of the job does the same at this
+// sync); the full plan until `reached` rounds are final again.
+int restore(Handle* h, int64_t reached) {
+    Ckpt& c = h->ck;
+    h->next_kernel = c.next_kernel;
+    int rc;
+    if ((rc = ckpt_copy(h, false))) return rc;
+    hipStream_t s = h->stream;
+    HIP_TRY(hipMemsetAsync(h->parts, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(h->pcount, 0, ((size_t)h->world + 2) * kSub * kCtrStride * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(h->overflow, 0, sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(h->pmax, 0, kMaxWorld * sizeof(uint32_t), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    h->rounds = c.rounds;
+    h->completed = c.completed;
+    h->converged = false;
+    h->k_launches = c.k_launches;
+    h->k_total_ms = c.k_total_ms;
+    h->k_aux_ms = c.k_aux_ms;
+    h->work_rounds = c.work_rounds;
+    h->timed_count = 0;
+    h->full_until = std::max(h->full_until, reached);
+    ++h->restores;
+    h->tiered = false;
+    h->delivered = 0;
+    full_plan(h);
+    return GP_OK;
+}
+
+// The next batch's plan (and a restore point when one is due), at a sync with no overflow.
+int choose_plan(Handle* h) {
+    // a sync with no round since the last one keeps the plan (the counters would disagree: this
+    // rank's were reset, the peers' last headers were not)
+    if (!h->delivered) return GP_OK;
+    h->delivered = 0;
+    const int W = h->world;
+    const bool tight = (h->cfg.flags & GP_FLAG_TIGHT_TIERS) != 0;
+    std::vector<uint32_t> mo((size_t)kMaxWorld, 0u), mi((size_t)W, 0u);
+    HIP_TRY(hipMemcpy(mo.data(), h->pmax, kMaxWorld * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (int q = 0; q < W && h->last_recv; ++q)
+        if (q != h->rank)
+            HIP_TRY(hipMemcpy(&mi[q], static_cast<const char*>(h->last_recv) + h->in_off[q] + offsetof(ShardHeader, runmax),
+                              sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemsetAsync(h->pmax, 0, kMaxWorld * sizeof(uint32_t), h->stream));
+    // global conditions only (every rank decides alike): half the nodes converged (the tail), no
+    // replay in progress, a batch already run
+    const bool on = !h->converged && h->last_recv && h->rounds >= h->full_until &&
+                    (tight || h->completed * 2 >= h->lay.nodes);
+    std::vector<uint32_t> oc((size_t)W), ic((size_t)W);
+    for (int q = 0; q < W; ++q) {
+        oc[q] = on ? tier_cap(h->full_out[q].cap, mo[q], tight) : h->full_out[q].cap;
+        ic[q] = on ? tier_cap(h->full_in[q].cap, mi[q], tight) : h->full_in[q].cap;
+    }
+    int rc;
+    if (on && (!h->ck.valid || tight || h->rounds - h->ck.rounds >= kCkptEvery)) {
+        if ((rc = ensure_ckpt(h)) || (rc = ckpt_copy(h, true))) return rc;
+    }
+    h->tiered = on;
+    bool changed = false;
+    for (int q = 0; q < W; ++q) changed |= oc[q] != h->out_chunk[q].cap || ic[q] != h->in_chunk[q].cap;
+    if (changed) {
+        apply_plan(h, oc, ic);
+        ++h->plan_changes;
+    }
     return GP_OK;
 }
 
@@ -992,8 +1216,23 @@ int shard_sync(Handle* h, gp_status* st) {
     uint32_t of = 0;
     HIP_TRY(hipMemcpy(&of, h->overflow, sizeof of, hipMemcpyDeviceToHost));
     if (of & 2u) return fail(GP_EOVERFLOW, "a shard received an entry outside its range; the run is void");
-    if (of) return fail(GP_EOVERFLOW, "a shard exchange buffer overflowed; the run is void");
     const int64_t applied = (int64_t)applied_round(h, h->next_kernel - 1) + 1;  // rounds whose counts exist
+    int rc;
+    if (of) {
+        // only a batch that may have run reduced chunks is replayed (every rank agrees on that); an
+        // overflow of the full plan is fatal, as its replay would overflow again
+        if (!(tiers_on(h) && h->tiered && h->ck.valid))
+            return fail(GP_EOVERFLOW, "a shard exchange buffer overflowed; the run is void");
+        if ((rc = restore(h, applied))) return rc;  // a reduced plan overflowed: replay with the full plan
+        if (st) {
+            std::memset(st, 0, sizeof *st);
+            st->round = h->rounds;
+            st->completed = h->completed;
+            st->converged = 0;
+            if ((rc = fill_sums(h, st))) return rc;
+        }
+        return GP_OK;
+    }
     int64_t timed_real = h->converged ? 0 : h->timed_count;  // after convergence no round is real
     if (!h->converged && applied > h->rounds) {
         const int64_t n = applied - h->rounds;
@@ -1011,10 +1250,10 @@ int shard_sync(Handle* h, gp_status* st) {
         timed_real = 0;  // sampled kernels that applied a real round (not past convergence)
         while (timed_real < h->timed_count && h->timed_round[(size_t)timed_real] < h->rounds) ++timed_real;
     }
-    int rc;
     if (h->timed_count && (rc = accumulate_timing(h, timed_real))) return rc;
     if (h->timed_count) h->work_rounds += timed_real;  // the quiet kernel counts in timed rounds only
     h->timed_count = 0;
+    if (tiers_on(h) && (rc = choose_plan(h))) return rc;
     if (st) {
         std::memset(st, 0, sizeof *st);
         st->round = h->rounds;
@@ -1754,6 +1993,24 @@ int gp_kernel_stats(void* handle, gp_kstats* out, int32_t reset_counters) {
         if (h->work)
             HIP_TRY(hipMemsetAsync(h->work, 0, (size_t)kParts * kWorkStride * sizeof *h->work, h->stream));
     }
+    return GP_OK;
+}
+
+int gp_shard_stats(void* handle, gp_shard_counters* out) {
+    if (!handle || !out) return fail(GP_EINVAL, "null argument");
+    Handle* h = H(handle);
+    if (h->grp) h = h->grp->shard[0];
+    if (!h->sharded) return fail(GP_ESTATE, "not a shard handle");
+    std::memset(out, 0, sizeof *out);
+    out->plan_changes = h->plan_changes;
+    out->restores = h->restores;
+    out->send_bytes = 0;
+    out->recv_bytes = 0;
+    for (int q = 0; q < h->world; ++q) {
+        out->send_bytes += (int64_t)h->out_chunk[q].size;
+        out->recv_bytes += (int64_t)h->in_chunk[q].size;
+    }
+    out->restore_round = h->ck.valid ? h->ck.rounds : -1;
     return GP_OK;
 }
 

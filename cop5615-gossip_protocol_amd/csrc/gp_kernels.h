@@ -127,8 +127,11 @@ struct RoundArgs {
 // full gossip: the target actor), then push-sum (s, w) pairs.  See DESIGN.md §6.
 struct ShardHeader {
     unsigned long long newly;  // actors that reported in the round (sender's range)
-    uint32_t overflow;         // sender dropped entries: the run is void (GP_EOVERFLOW)
-    uint32_t pad;
+    uint32_t overflow;         // sender dropped entries: the run is void (GP_EOVERFLOW) unless a
+                               // checkpoint restores it (activity tiers, gp_api.cpp)
+    uint32_t runmax;           // the sender's most link entries in one sub-segment of its chunk to
+                               // this peer, over the rounds since the plan was last chosen: both
+                               // ends size the next batch's chunk from it
     uint32_t nlinks[kSub];     // link entries written per sub-segment (<= cap)
     uint32_t nhalo[kSub];      // halo entries written per sub-segment (<= hcap)
 };
@@ -171,6 +174,8 @@ struct Xchg {
                                    // halo side, sub), kCtrStride apart (zeroed by pack)
     uint32_t* overflow;            // sticky local overflow flag
     unsigned long long* self_newly;  // this rank's count of the round (pack -> unpack)
+    uint32_t* pmax;                // [kMaxWorld] running max of link entries per sub-segment to each
+                                   // peer (reset when the host chooses the plan)
     PeerOut out[kMaxWorld];
     PeerIn in[kMaxWorld];
     HaloX h;

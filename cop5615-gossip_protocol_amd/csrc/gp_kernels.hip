@@ -1159,7 +1159,7 @@ static_assert(kMaxWorld * kSub == kBlock, "k_shard_pack maps one thread per (pee
 
 __global__ __launch_bounds__(kBlock) void k_shard_pack(RoundArgs a, Xchg x, long long applied) {
     __shared__ unsigned long long newly_s;
-    __shared__ uint32_t of_s[kMaxWorld];
+    __shared__ uint32_t of_s[kMaxWorld], max_s[kMaxWorld];
     if (threadIdx.x < 64) {
         unsigned long long newly = 0;
         if (applied >= 0) newly = *part_slot(a.parts, applied, threadIdx.x);
@@ -1170,7 +1170,10 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(RoundArgs a, Xchg x, long
             newly_s = newly;
         }
     }
-    if (threadIdx.x < kMaxWorld) of_s[threadIdx.x] = 0u;
+    if (threadIdx.x < kMaxWorld) {
+        of_s[threadIdx.x] = 0u;
+        max_s[threadIdx.x] = 0u;
+    }
     __syncthreads();
     const uint32_t q = threadIdx.x / kSub, s = threadIdx.x % kSub;
     const bool peer = q < x.world && q != x.rank;
@@ -1179,6 +1182,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(RoundArgs a, Xchg x, long
         uint32_t* lc = ctr_at(x, q, s);
         const uint32_t c = *lc;
         hd->nlinks[s] = c < x.out[q].cap ? c : x.out[q].cap;
+        atomicMax(&max_s[q], c);
         bool of = c > x.out[q].cap;
         *lc = 0u;
         const int side = q + 1 == x.rank ? 0 : q == x.rank + 1 ? 1 : -1;
@@ -1197,7 +1201,9 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(RoundArgs a, Xchg x, long
     if (peer && s == 0) {
         hd->newly = newly_s;
         hd->overflow = (of_s[q] || *x.overflow) ? 1u : 0u;
-        hd->pad = 0u;
+        const uint32_t m = max_s[q] > x.pmax[q] ? max_s[q] : x.pmax[q];  // one writer per peer
+        x.pmax[q] = m;
+        hd->runmax = m;
     }
 }
 

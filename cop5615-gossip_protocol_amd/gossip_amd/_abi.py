@@ -13,7 +13,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, os.environ.get("GP_LIB", "lib"), "libgossip_hip.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "gossip_hip.h")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 TOPOLOGIES = {"line": 0, "full": 1, "2D": 2, "Imp3D": 3, "3D": 4}
 ALGOS = {"gossip": 0, "push-sum": 1}
 FLAG_KERNEL_TIMING = 1
@@ -23,6 +23,8 @@ FLAG_ONE_DEVICE = 8
 FLAG_GROUP = 16
 FLAG_QUIET_WAVES = 32
 FLAG_GOSSIP_TALLY = 64
+FLAG_FULL_PLAN = 128
+FLAG_TIGHT_TIERS = 256
 ERRORS = {-1: "GP_EINVAL", -2: "GP_ENOMEM", -3: "GP_EHIP", -4: "GP_ESTATE", -5: "GP_EOVERFLOW", -6: "GP_ERCCL"}
 
 
@@ -56,10 +58,15 @@ class ShardLayout(C.Structure):
                 ("send_total", C.c_int64), ("recv_total", C.c_int64)]
 
 
+class ShardStats(C.Structure):
+    _fields_ = [("plan_changes", C.c_int64), ("restores", C.c_int64), ("send_bytes", C.c_int64),
+                ("recv_bytes", C.c_int64), ("restore_round", C.c_int64)]
+
+
 EXPORTS = ["gp_abi_version", "gp_sizes", "gp_create", "gp_reset", "gp_step", "gp_read_gossip",
            "gp_read_pushsum", "gp_read_messages", "gp_read_trace", "gp_neighbors",
            "gp_kernel_stats", "gp_partition", "gp_create_shard", "gp_shard_plan", "gp_shard_round",
-           "gp_shard_deliver", "gp_shard_sync", "gp_destroy", "gp_last_error"]
+           "gp_shard_deliver", "gp_shard_sync", "gp_shard_stats", "gp_destroy", "gp_last_error"]
 
 
 class GossipError(RuntimeError):
@@ -102,6 +109,7 @@ def load():
     L.gp_shard_round.argtypes = [P, P]
     L.gp_shard_deliver.argtypes = [P, P]
     L.gp_shard_sync.argtypes = [P, C.POINTER(Status)]
+    L.gp_shard_stats.argtypes = [P, C.POINTER(ShardStats)]
     L.gp_destroy.argtypes = [P]
     L.gp_destroy.restype = None
     L.gp_last_error.restype = C.c_char_p

@@ -6,11 +6,14 @@ the actors on the .NET thread pool (program.fs:23), and the ParentActor counts r
 (``gp_partition``: whole z-planes for Imp3D/3D) and one round is
 
     engine.round()          # F(k) on this rank's actors + pack what other ranks need
-    transport.exchange()    # ONE all-to-all with sizes fixed at creation (RCCL over xGMI)
+    transport.exchange()    # ONE all-to-all (RCCL over xGMI); chunk sizes change only at a sync
     engine.deliver()        # unpack: halo faces, cross-shard link messages, global count
 
 with everything enqueued on the engine's HIP stream — the host only waits every few rounds
-(``engine.sync()``) to learn whether the global completion count reached `nodes`.
+(``engine.sync()``) to learn whether the global completion count reached `nodes`.  At that sync
+a push-sum shard also sizes the next batch's chunks from the activity of the last one (activity
+tiers, gp_shard_plan), and may rewind to a restore point if a reduced chunk overflowed: the host
+loop just runs on from the round the sync reports.
 
 Engines: :class:`HipShard` (libgossip_hip.so on a GPU — the product) and, in the tests,
 ``oracle.OracleShard`` (the CPU checker).  Transports: :class:`TorchTransport`
@@ -39,9 +42,12 @@ class HipShard:
 
     def __init__(self, n_arg: int, topology: str, algorithm: str, *, rank: int, world: int, seed: int = 1,
                  device: int = 0, stream: int | None = None, kernel_timing: bool = False, delta: float = 1e-10,
-                 gossip_threshold: int = 10, term_init: int = 1, term_limit: int = 3, quiet_waves: bool = False):
+                 gossip_threshold: int = 10, term_init: int = 1, term_limit: int = 3, quiet_waves: bool = False,
+                 full_plan: bool = False, tight_tiers: bool = False):
         """quiet_waves: the push-sum quiet-tail walk at any shard size (a test hook; on by default
-        for shards of 2^20 actors or more)."""
+        for shards of 2^20 actors or more).  full_plan: no activity tiers (every round ships the
+        all-sending capacity); tight_tiers: tiers with no headroom and frequent replays (a test
+        hook)."""
         import torch
 
         if topology not in _abi.TOPOLOGIES:
@@ -53,6 +59,7 @@ class HipShard:
         # kernels; its handle may be 0 (the null stream), hence FLAG_USE_STREAM
         flags = (_abi.FLAG_KERNEL_TIMING if kernel_timing else 0) | _abi.FLAG_USE_STREAM
         flags |= _abi.FLAG_QUIET_WAVES if quiet_waves else 0
+        flags |= (_abi.FLAG_FULL_PLAN if full_plan else 0) | (_abi.FLAG_TIGHT_TIERS if tight_tiers else 0)
         if stream is None:
             stream = torch.cuda.current_stream(device).cuda_stream
         self.cfg = _abi.Config(n_arg, _abi.TOPOLOGIES[topology], _abi.ALGOS[algorithm], seed, delta,
@@ -66,15 +73,28 @@ class HipShard:
         self.rank, self.world = rank, world
         self.topology, self.algorithm = topology, algorithm
         self.lo, self.hi = int(self.shard.lo), int(self.shard.hi)
-        sb = np.zeros(world, np.int64)
-        rb = np.zeros(world, np.int64)
+        self._plan()
+        dev = torch.device("cuda", device)
+        # buffers for the full plan (the first one); the caching allocator hands out 512-byte
+        # aligned blocks (the ABI needs 256)
+        st, rt = int(self.shard.send_total), int(self.shard.recv_total)
+        self.send_buf = torch.zeros(max(1, st), dtype=torch.uint8, device=dev)[:st]
+        self.recv_buf = torch.zeros(max(1, rt), dtype=torch.uint8, device=dev)[:rt]
+        self.status = _abi.Status()
+
+    def _plan(self):
+        """The current per-peer chunk sizes (gp_shard_plan): they follow the activity of the run
+        (activity tiers) and are re-read after every sync."""
+        sb = np.zeros(self.world, np.int64)
+        rb = np.zeros(self.world, np.int64)
         _abi.check(self.lib.gp_shard_plan(self.h, sb.ctypes.data_as(C.c_void_p), rb.ctypes.data_as(C.c_void_p)))
         self.send_splits, self.recv_splits = [int(x) for x in sb], [int(x) for x in rb]
-        dev = torch.device("cuda", device)
-        # the caching allocator hands out 512-byte aligned blocks (the ABI needs 256)
-        self.send_buf = torch.zeros(max(1, int(sb.sum())), dtype=torch.uint8, device=dev)[: int(sb.sum())]
-        self.recv_buf = torch.zeros(max(1, int(rb.sum())), dtype=torch.uint8, device=dev)[: int(rb.sum())]
-        self.status = _abi.Status()
+
+    def shard_stats(self):
+        s = _abi.ShardStats()
+        _abi.check(self.lib.gp_shard_stats(self.h, C.byref(s)))
+        return {"plan_changes": s.plan_changes, "restores": s.restores, "send_bytes": s.send_bytes,
+                "recv_bytes": s.recv_bytes, "restore_round": s.restore_round}
 
     @property
     def nodes(self) -> int:
@@ -92,11 +112,13 @@ class HipShard:
 
     def sync(self):
         _abi.check(self.lib.gp_shard_sync(self.h, C.byref(self.status)))
+        self._plan()
         return self.status
 
     def reset(self):
         _abi.check(self.lib.gp_reset(self.h))
         self.status = _abi.Status()
+        self._plan()
 
     # read-back of this rank's actors [lo, hi) (global ids)
     def read_gossip(self):
@@ -155,8 +177,9 @@ class HipShard:
 
 class TorchTransport:
     """The per-round exchange as one torch.distributed all_to_all_single: RCCL over xGMI for
-    device buffers (backend "nccl" on ROCm), gloo for CPU buffers.  Sizes never change, so
-    there is no count exchange and no host synchronisation inside a round."""
+    device buffers (backend "nccl" on ROCm), gloo for CPU buffers.  Sizes change only at a sync
+    (the engine's plan), so there is no count exchange and no host synchronisation inside a
+    round."""
 
     def __init__(self, group=None):
         import torch.distributed as dist
@@ -165,7 +188,9 @@ class TorchTransport:
         self.group = group
 
     def exchange(self, eng):
-        self.dist.all_to_all_single(eng.recv_buf, eng.send_buf, eng.recv_splits, eng.send_splits,
+        # the current plan's chunks are packed from offset 0 (a prefix of the full-plan buffers)
+        ns, nr = sum(eng.send_splits), sum(eng.recv_splits)
+        self.dist.all_to_all_single(eng.recv_buf[:nr], eng.send_buf[:ns], eng.recv_splits, eng.send_splits,
                                     group=self.group)
 
 

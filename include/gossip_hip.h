@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 4
+#define GP_ABI_VERSION 5
 
 /* program.fs:151 "line", :191 "full", :227 "2D", :267 "Imp3D"; "3D" is build-defined (Q9) */
 enum gp_topology { GP_LINE = 0, GP_FULL = 1, GP_TWO_D = 2, GP_IMP3D = 3, GP_THREE_D = 4 };
@@ -54,6 +54,10 @@ enum gp_flags {
     GP_FLAG_GOSSIP_TALLY = 64, /* full gossip, one GPU: tally receipts by target bucket in every
                                   round from round 1 at any graph size (default: from 2^20 actors,
                                   after a round with many chains); a test hook, same results */
+    GP_FLAG_FULL_PLAN = 128,   /* push-sum shards: keep the full exchange plan (no activity tiers) */
+    GP_FLAG_TIGHT_TIERS = 256, /* push-sum shards: activity tiers from the first batch with no
+                                  headroom and a restore point at every sync, so reduced chunks
+                                  overflow and batches replay often; a test hook, same results */
 };
 
 typedef struct gp_config {
@@ -171,7 +175,12 @@ typedef struct gp_shard_layout {
  * topology, push-sum on line/2D/Imp3D/3D (push-sum on "full" is single-GPU only). */
 int gp_create_shard(const gp_config* cfg, int32_t rank, int32_t world, gp_layout* out,
                     gp_shard_layout* shard, void** handle);
-/* Per-peer byte counts of the send and receive buffers (arrays of `world`; peer order). */
+/* Per-peer byte counts of the current exchange (arrays of `world`; peer order): chunk p -> q is
+ * sent_bytes[q] bytes at the running offset of the send buffer, and likewise for the receive
+ * buffer.  The buffers are allocated for the full plan (gp_shard_layout send_total / recv_total);
+ * push-sum shards size each batch's chunks from the activity of the batch before (activity tiers:
+ * the converged tail ships a fraction of an all-sending round), so a host re-reads the plan after
+ * every gp_shard_sync.  Both ends of a chunk always agree on its size. */
 int gp_shard_plan(void* handle, int64_t* send_bytes, int64_t* recv_bytes);
 /* Enqueue one round on the handle's stream and pack what other ranks need into send_buf
  * (device memory, send_total bytes, 256-byte aligned).  Asynchronous. */
@@ -180,8 +189,21 @@ int gp_shard_round(void* handle, void* send_buf);
  * bytes of device memory).  Must follow each gp_shard_round.  Asynchronous. */
 int gp_shard_deliver(void* handle, const void* recv_buf);
 /* Wait for the enqueued rounds and fill st from the global completion counts (st->sum_s /
- * sum_w are this rank's share).  Fails with GP_EOVERFLOW if a link buffer overflowed. */
+ * sum_w are this rank's share), then choose the next batch's plan (gp_shard_plan).  If a reduced
+ * (activity-tier) chunk overflowed in the batch, every rank discards the batch and returns to its
+ * restore point: st->round goes back to that round and the host simply runs on from there (the
+ * run stays exact).  Fails with GP_EOVERFLOW if a full-plan buffer overflowed. */
 int gp_shard_sync(void* handle, gp_status* st);
+
+typedef struct gp_shard_counters {
+    int64_t plan_changes;   /* exchange plans chosen since creation (activity tiers)            */
+    int64_t restores;       /* overflowed batches replayed from a restore point                 */
+    int64_t send_bytes;     /* bytes of the current plan's send / receive chunks                */
+    int64_t recv_bytes;
+    int64_t restore_round;  /* round of the current restore point (-1: none)                     */
+} gp_shard_counters;
+/* Exchange-plan counters of a shard (num_gpus > 1 handle: rank 0's). */
+int gp_shard_stats(void* handle, gp_shard_counters* out);
 
 void gp_destroy(void* handle);
 

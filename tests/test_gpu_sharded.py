@@ -134,12 +134,20 @@ QUIET_SHARD_CASES = [
 ]
 
 
+@pytest.mark.parametrize("tiers", ["default", "tight"])
 @pytest.mark.parametrize("n,topo,world,seed", QUIET_SHARD_CASES)
-def test_shards_quiet_tail_vs_oracle(n, topo, world, seed):
+def test_shards_quiet_tail_vs_oracle(n, topo, world, seed, tiers):
+    """tight: activity tiers from the first batch with no headroom (GP_FLAG_TIGHT_TIERS), so reduced
+    chunks overflow and batches are discarded and replayed from restore points over and over: the
+    run must still be exact."""
     ref = oracle.OracleSim(n, topo, "push-sum", seed=seed)
     rs = ref.step(1 << 20, threads=8)
-    engines = _shards(n, topo, "push-sum", world, seed, quiet_waves=True)
+    engines = _shards(n, topo, "push-sum", world, seed, quiet_waves=True, tight_tiers=tiers == "tight")
     sts = sharded.run_local(engines, max_rounds=1 << 20)
+    if tiers == "tight" and n >= 200000:
+        ss = [e.shard_stats() for e in engines]
+        assert all(x["plan_changes"] > 0 for x in ss), ss
+        assert sum(x["restores"] for x in ss) > 0, ss
     assert rs.converged
     for st in sts:
         assert (st.round, st.completed, st.converged) == (rs.round, rs.completed, rs.converged)
@@ -167,6 +175,15 @@ def _quiet_shard_sweep(count=16, seed=99):
 
 @pytest.mark.parametrize("n,topo,world,seed", _quiet_shard_sweep())
 def test_shards_quiet_tail_random_sweep(n, topo, world, seed):
+    _quiet_sweep_case(n, topo, world, seed, tight=False)
+
+
+@pytest.mark.parametrize("n,topo,world,seed", _quiet_shard_sweep(count=12, seed=1234))
+def test_shards_tight_tiers_random_sweep(n, topo, world, seed):
+    _quiet_sweep_case(n, topo, world, seed, tight=True)
+
+
+def _quiet_sweep_case(n, topo, world, seed, tight):
     try:
         sharded.partition(n, topo, world)
     except GossipError as e:
@@ -175,7 +192,7 @@ def test_shards_quiet_tail_random_sweep(n, topo, world, seed):
         pytest.skip(str(e))
     ref = oracle.OracleSim(n, topo, "push-sum", seed=seed)
     rs = ref.step(1 << 20, threads=8)
-    engines = _shards(n, topo, "push-sum", world, seed, quiet_waves=True)
+    engines = _shards(n, topo, "push-sum", world, seed, quiet_waves=True, tight_tiers=tight)
     sts = sharded.run_local(engines, max_rounds=int(rs.round))
     for st in sts:
         assert (st.round, st.completed, st.converged) == (rs.round, rs.completed, rs.converged)
@@ -201,6 +218,57 @@ def test_shards_quiet_default_and_work_count():
         assert ks["launches"] == (int(rs.round) + 7) // 8, ks  # every 8th round is timed
         assert 0 < ks["work_per_launch"] < e.hi - e.lo, ks
         e.close()
+
+
+def test_shards_activity_tiers_default():
+    """Default activity tiers on an 8-rank run to convergence (2M Imp3D, 7/8 of the links remote):
+    once half the nodes have converged, each batch's chunks are sized from the last batch's counts,
+    so the tail ships a fraction of the full plan; bit-exact against the single-GPU engine and
+    against the same shards with the full plan."""
+    n, seed = 2_000_000, 7
+    ref = Simulator(n, "Imp3D", "push-sum", seed=seed)
+    rs = ref.step()
+    engines = _shards(n, "Imp3D", "push-sum", 8, seed)
+    full_bytes = sum(engines[0].send_splits)
+    t = sharded.LoopbackTransport()
+    sts = [e.sync() for e in engines]
+    least, batch = full_bytes, 8
+    while not sts[0].converged:
+        for _ in range(batch):
+            for e in engines:
+                e.round()
+            t.exchange_all(engines)
+            for e in engines:
+                e.deliver()
+        sts = [e.sync() for e in engines]
+        least = min(least, sum(engines[0].send_splits))
+        batch = min(batch * 2, 64)
+    assert (sts[0].round, sts[0].completed) == (rs.round, rs.completed)
+    _check_vs(ref, engines, "push-sum")
+    ss = [e.shard_stats() for e in engines]
+    assert all(x["plan_changes"] > 0 for x in ss), ss
+    assert least * 4 < full_bytes, (least, full_bytes)
+    for e in engines:
+        e.close()
+
+
+@pytest.mark.parametrize("n,topo,world,seed", [(20000, "Imp3D", 3, 5), (300000, "Imp3D", 8, 11)])
+def test_group_tight_tiers_vs_oracle(n, topo, world, seed):
+    """The library's multi-GPU engine (gp_step over num_gpus shards, here on one device) with
+    tight tiers: its own exchange follows the plans and replays overflowed batches."""
+    gpu = Simulator(n, topo, "push-sum", seed=seed, num_gpus=world, one_device=True, quiet_waves=True,
+                    tight_tiers=True)
+    cpu = oracle.OracleSim(n, topo, "push-sum", seed=seed)
+    gs, cs = gpu.step(), cpu.step(1 << 20, threads=8)
+    assert gs.converged and (gs.round, gs.completed) == (cs.round, cs.completed)
+    S, W, f = gpu.read_pushsum()
+    rS, rW, rf = cpu.read_pushsum()
+    np.testing.assert_array_equal(f, rf)
+    np.testing.assert_array_equal(bits(S), bits(rS))
+    np.testing.assert_array_equal(bits(W), bits(rW))
+    np.testing.assert_array_equal(gpu.read_trace(), cpu.read_trace())
+    gpu.close()
+    cpu.close()
 
 
 def test_shards_imp3d_10m_two_ranks():
