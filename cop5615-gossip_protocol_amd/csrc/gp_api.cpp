@@ -1099,9 +1099,8 @@ int ensure_ckpt(Handle* h) {
     const size_t xn = (size_t)(h->ext_hi() - h->ext_lo()), n = h->own();
     const size_t nsl = (size_t)(h->sbnd.empty() ? 0 : h->sbnd[h->rank + 1] - h->sbnd[h->rank]);
     int rc;
-    if ((rc = h->alloc(&c.msg, xn)) || (rc = h->alloc(&c.dir, xn)) || (rc = h->alloc(&c.flags, n)) ||
-        (rc = h->alloc(&c.work, (size_t)kParts * kWorkStride)))
-        return rc;
+    if ((rc = h->alloc(&c.msg, xn)) || (rc = h->alloc(&c.dir, xn)) || (rc = h->alloc(&c.flags, n))) return rc;
+    if (h->work && (rc = h->alloc(&c.work, (size_t)kParts * kWorkStride))) return rc;
     if (h->lcnt[0] && ((rc = h->alloc(&c.lcnt, nsl)) || (rc = h->alloc(&c.rmsg, nsl)))) return rc;
     if (h->act[0] && (rc = h->alloc(&c.act, act_bytes(h)))) return rc;
     return GP_OK;
@@ -1121,7 +1120,7 @@ int ckpt_copy(Handle* h, bool save) {
     HIP_TRY(cp(h->msg[p] + xlo, c.msg, xn * sizeof(double2)));
     HIP_TRY(cp(h->dir[p] + xlo, c.dir, xn));
     HIP_TRY(cp(h->flags + lo, c.flags, n));
-    HIP_TRY(cp(h->work, c.work, (size_t)kParts * kWorkStride * sizeof *h->work));
+    if (h->work) HIP_TRY(cp(h->work, c.work, (size_t)kParts * kWorkStride * sizeof *h->work));
     if (h->lcnt[0]) {
         const size_t slo = (size_t)h->sbnd[h->rank], nsl = (size_t)(h->sbnd[h->rank + 1] - h->sbnd[h->rank]);
         HIP_TRY(cp(h->lcnt[p] + slo, c.lcnt, nsl));
