@@ -247,7 +247,7 @@ def test_shards_activity_tiers_default():
     _check_vs(ref, engines, "push-sum")
     ss = [e.shard_stats() for e in engines]
     assert all(x["plan_changes"] > 0 for x in ss), ss
-    assert least * 4 < full_bytes, (least, full_bytes)
+    assert least * 2 < full_bytes, (least, full_bytes)  # the fixed halo part and the 64-entry floor remain
     for e in engines:
         e.close()
 
