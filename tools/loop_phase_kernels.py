@@ -1,0 +1,50 @@
+"""Per-kernel cost of one rank-round by phase of a loopback shard run (tools/shard_loopback_prof.py
+under rocprofv3 --kernel-trace): the dispatches are assigned to rounds by counting the round
+kernel's launches (world per round, after the 8 warm-up rounds), and each round to a phase by the
+global completion count before it (the run's trace from --series).
+
+    python3 tools/loop_phase_kernels.py KT_CSV SERIES_JSON ROUND_KERNEL [world]
+"""
+import csv
+import json
+import statistics
+import sys
+from collections import defaultdict
+
+
+def name(r):
+    return r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("gp::", "")
+
+
+def main():
+    kt, series, rk = sys.argv[1:4]
+    world = int(sys.argv[4]) if len(sys.argv) > 4 else 8
+    d = json.load(open(series))
+    trace, nodes = d["trace"], None
+    rows = sorted(csv.DictReader(open(kt)), key=lambda r: int(r["Start_Timestamp"]))
+    seen, rnd = 0, -1
+    per = defaultdict(lambda: defaultdict(float))  # round -> kernel -> us (all ranks)
+    for r in rows:
+        n = name(r)
+        if n == rk:
+            seen += 1
+            rnd = (seen - 1) // world - 8  # 8 warm-up rounds
+        if rnd < 0:
+            continue
+        per[rnd][n] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    nodes = d.get("nodes") or max(trace)
+    prev = [0] + trace[:-1]
+    phases = {"dense (<1% converged)": lambda c: c * 100 < nodes, "tail (>=99% converged)": lambda c: c * 100 >= 99 * nodes}
+    for label, test in phases.items():
+        rs = [r for r in per if r < len(prev) and test(prev[r])]
+        if not rs:
+            continue
+        ks = sorted({k for r in rs for k in per[r]}, key=lambda k: -sum(per[r].get(k, 0.0) for r in rs))
+        tot = statistics.fmean(sum(per[r].values()) for r in rs) / world
+        print(f"{label}: {len(rs)} rounds, kernels per rank-round {tot:.1f} us")
+        for k in ks:
+            print(f"  {k:48s} {statistics.fmean(per[r].get(k, 0.0) for r in rs) / world:9.2f} us")
+
+
+if __name__ == "__main__":
+    main()

@@ -47,21 +47,31 @@ cap = a.rounds if a.rounds else 1 << 40
 t = sharded.LoopbackTransport()
 events = []
 sts = [e.sync() for e in shards]
+send_bytes = [(0, sum(shards[0].send_splits))]
 batch = 8
 t0 = time.perf_counter()
 while not sts[0].converged and sts[0].round < cap:
     for _ in range(min(batch, cap - int(sts[0].round))):
-        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        # the whole round, and rank 0's own work in it: its round kernels + passes, the chunk
+        # copies of every rank, its unpack
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
         ev[0].record()
-        for e in shards:
+        for i, e in enumerate(shards):
             e.round()
+            if i == 0:
+                ev[1].record()
+        ev[2].record()
         t.exchange_all(shards)
-        for e in shards:
+        ev[3].record()
+        for i, e in enumerate(shards):
             e.deliver()
-        ev[1].record()
+            if i == 0:
+                ev[4].record()
+        ev[5].record()
         events.append(ev)
     sts = [e.sync() for e in shards]
     assert len({(int(s.round), int(s.completed), int(s.converged)) for s in sts}) == 1, "shards disagree"
+    send_bytes.append((int(sts[0].round), sum(shards[0].send_splits)))  # rank 0's plan from here on
     batch = min(batch * 2, 64)
 torch.cuda.synchronize()
 el = time.perf_counter() - t0
@@ -69,7 +79,11 @@ rounds = int(sts[0].round)
 trace = [int(x) for x in shards[0].read_trace()]
 # gossip's F(k) applies round k - 1: one launch more than rounds
 launches = rounds + (1 if a.algorithm == "gossip" else 0)
-per_round = [events[i][0].elapsed_time(events[i][1]) for i in range(min(launches, len(events)))]
+nl = min(launches, len(events))
+per_round = [events[i][0].elapsed_time(events[i][5]) for i in range(nl)]
+# rank 0 without the transport: its round (kernel + passes + pack) and its unpack
+rank0 = [events[i][0].elapsed_time(events[i][1]) + events[i][3].elapsed_time(events[i][4]) for i in range(nl)]
+copies = [events[i][2].elapsed_time(events[i][3]) for i in range(nl)]
 ks = shards[0].kernel_stats()
 
 
@@ -77,27 +91,43 @@ def mean(xs):
     return statistics.fmean(xs) if xs else None
 
 
-# round r is "all-sending" while no node had converged after round r - 1; "tail" once 99% had
+# round r is "dense" while fewer than 1% of the nodes had converged after round r - 1 (nearly every
+# actor sends), "tail" once 99% had
 prev = [0] + trace[:-1]
-dense = [per_round[r] for r in range(len(per_round)) if r < len(prev) and prev[r] == 0]
-tail = [per_round[r] for r in range(len(per_round)) if r < len(prev) and prev[r] * 100 >= 99 * nodes]
+dense_r = [r for r in range(nl) if r < len(prev) and prev[r] * 100 < nodes]
+tail_r = [r for r in range(nl) if r < len(prev) and prev[r] * 100 >= 99 * nodes]
+
+
+def phase(xs, rs, div=1.0):
+    return mean([xs[r] for r in rs]) / div if rs else None
+
+
 summary = {
     "workload": f"{a.n} {a.topology} {a.algorithm}", "world": a.world, "rounds": rounds,
     "converged": bool(sts[0].converged), "host_ms": el * 1e3,
     "round_ms_sum": sum(per_round),
-    "rank_round_ms_all_sending": mean(dense) / a.world if dense else None,
-    "rank_round_ms_tail_99": mean(tail) / a.world if tail else None,
-    "tail_over_all_sending": (mean(tail) / mean(dense)) if dense and tail else None,
-    "rounds_all_sending": len(dense), "rounds_tail_99": len(tail),
+    "rounds_dense_lt1pct": len(dense_r), "rounds_tail_99pct": len(tail_r),
+    # one round of all ranks / world (rank kernels serialised + every chunk copy)
+    "rank_round_ms_dense": phase(per_round, dense_r, a.world),
+    "rank_round_ms_tail": phase(per_round, tail_r, a.world),
+    "tail_over_dense": phase(per_round, tail_r) / phase(per_round, dense_r) if dense_r and tail_r else None,
+    # rank 0's own kernels per round (no transport: on a real node its all-to-all runs in parallel)
+    "rank0_ms_dense": phase(rank0, dense_r), "rank0_ms_tail": phase(rank0, tail_r),
+    "rank0_tail_over_dense": phase(rank0, tail_r) / phase(rank0, dense_r) if dense_r and tail_r else None,
+    "copies_ms_dense": phase(copies, dense_r), "copies_ms_tail": phase(copies, tail_r),
     "rank0_kernel": ks["kernel"], "rank0_kernel_avg_ms": ks["avg_ms"], "rank0_aux": ks["aux_kernel"],
     "rank0_aux_avg_ms": ks["aux_avg_ms"], "rank0_work_per_launch": ks["work_per_launch"],
     "rank0_actors": shards[0].hi - shards[0].lo,
-    "bytes_sent_per_round_rank0": sum(shards[0].send_splits),
+    "send_bytes_rank0_full_plan": send_bytes[0][1],
+    "send_bytes_rank0_least": min(b for _, b in send_bytes),
+    "shard_stats_rank0": shards[0].shard_stats(),
     "note": "all ranks serialised on one GPU; exchange = device copies (no RCCL); rank-round = round / world",
 }
 print(json.dumps(summary, indent=1), flush=True)
 if a.series:
     with open(a.series, "w") as f:
-        json.dump(dict(summary, per_round_ms=[round(x, 4) for x in per_round], trace=trace), f)
+        json.dump(dict(summary, per_round_ms=[round(x, 4) for x in per_round],
+                       rank0_ms=[round(x, 4) for x in rank0], copies_ms=[round(x, 4) for x in copies],
+                       send_bytes=send_bytes, trace=trace), f)
 for e in shards:
     e.close()
