@@ -165,6 +165,7 @@ struct Handle {
     uint32_t* lpos = nullptr;
     uint8_t* lcnt[2] = {nullptr, nullptr};   // gossip link slots
     double2* rmsg[2] = {nullptr, nullptr};   // shards, push-sum: remote senders' link messages per CSR slot
+    uint32_t* slot_dst = nullptr;            // shards with the quiet tail: receiver of each own CSR slot
     // push-sum
     double2* msg[2] = {nullptr, nullptr};
     uint8_t* dir[2] = {nullptr, nullptr};
@@ -391,6 +392,13 @@ int build_links(Handle* h) {
         if (h->sharded && h->world > 1 && !h->gossip &&
             ((rc = h->alloc(&h->rmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->rmsg[1], (size_t)nsl, slo))))
             return rc;
+        // the unpack marks the segment of a remote link message's receiver (quiet tail)
+        if (h->sharded && h->world > 1 && !h->gossip && h->act[0]) {
+            if ((rc = h->alloc(&h->slot_dst, (size_t)nsl, slo))) return rc;
+            launch_slot_owner(h->rev_off, lo, hi, h->slot_dst, h->L());
+            HIP_TRY(hipStreamSynchronize(s));
+            HIP_TRY(hipGetLastError());
+        }
     }
     if (h->sharded) {  // link counts per (source rank, destination rank, sender degree)
         const size_t nb = (size_t)h->world * h->world * 8;
@@ -962,6 +970,7 @@ Xchg base_xchg(const Handle* h) {
     x.overflow = h->overflow;
     x.self_newly = h->self_newly;
     x.pmax = h->pmax;
+    x.slot_dst = h->slot_dst;
     return x;
 }
 

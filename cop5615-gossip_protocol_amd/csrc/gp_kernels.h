@@ -176,6 +176,8 @@ struct Xchg {
     unsigned long long* self_newly;  // this rank's count of the round (pack -> unpack)
     uint32_t* pmax;                // [kMaxWorld] running max of link entries per sub-segment to each
                                    // peer (reset when the host chooses the plan)
+    const uint32_t* slot_dst;      // push-sum, quiet tail: the receiver of each own link slot (the
+                                   // unpack marks the segment of a remote link message's receiver)
     PeerOut out[kMaxWorld];
     PeerIn in[kMaxWorld];
     HaloX h;
@@ -254,6 +256,8 @@ void launch_dst_fill(uint64_t seed, uint32_t nodes, uint32_t ulo, uint32_t uhi, 
                      const uint32_t* off, uint32_t* fill, uint32_t* out, const Launch& l);
 void launch_add_u32(uint32_t* x, const uint32_t* y, uint32_t n, const Launch& l);
 void launch_sort_segments(const uint32_t* off, uint32_t* vals, uint32_t n, const Launch& l);
+// dst[s] = v for every slot s of the CSR segments of actors [lo, hi)
+void launch_slot_owner(const uint32_t* off, uint32_t lo, uint32_t hi, uint32_t* dst, const Launch& l);
 void launch_lpos_lists(const uint32_t* off, const uint32_t* list, uint32_t nt, const uint32_t* base, uint32_t* lpos,
                        const Launch& l);
 // exclusive scan of n u32 counts into off[0..n]; scratch >= scan_scratch_words(n) u32

@@ -1044,6 +1044,16 @@ __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg 
     if (applied_converged(a)) return;  // block-uniform: F(r) was a no-op
     const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
     const uint32_t base = a.lo + blockIdx.x * kBlock * kShardPer + threadIdx.x;
+    // Quiet tail: F(r) walked only the segments marked link_tag(r) in act_prev, and every actor it
+    // did not walk sends nothing; a block whose kShardPer * kBlock actors lie in unmarked segments
+    // has no message to route (most blocks of the tail: 33 -> a few us per rank-round at 100M / 8).
+    if (a.act_prev && a.r >= 2u && a.total[a.r - 2u] >= a.act_thr) {
+        static_assert(kShardPer * kBlock / kActSeg == kBlock, "one segment mark per thread (+1)");
+        const uint32_t s0 = (base - threadIdx.x) >> kActShift;
+        bool any = a.act_prev[s0 + threadIdx.x] == (uint8_t)a.tag_cur;
+        if (threadIdx.x == 0) any = any || a.act_prev[s0 + kBlock] == (uint8_t)a.tag_cur;
+        if (!__syncthreads_or(any)) return;  // block-uniform
+    }
     const uint32_t slo = x.sbnd[x.rank], shi = x.sbnd[x.rank + 1];
     bool l[kShardPer];
 #pragma unroll
@@ -1275,15 +1285,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
                 a.rmsg_cur[t] = in.msg[i];
                 a.lcnt_cur[t] = (uint8_t)a.tag_cur;  // plain: non-temporal marks and messages
                                                      // cost 0.29 ms more per round (C5 / 8)
-                if (mark) {  // the receiver owning slot t: the last v in [lo, hi) with rev_off[v] <= t
-                    uint32_t l = a.lo, h = a.hi;
-                    while (h - l > 1u) {
-                        const uint32_t mid = l + ((h - l) >> 1);
-                        if (a.rev_off[mid] <= t) l = mid;
-                        else h = mid;
-                    }
-                    a.act_cur[l >> kActShift] = mtag;
-                }
+                if (mark) a.act_cur[x.slot_dst[t] >> kActShift] = mtag;  // the receiver owning slot t
             }
         }
     }
@@ -1832,6 +1834,11 @@ __global__ void k_lpos_lists(const uint32_t* off, const uint32_t* list, uint32_t
         for (uint32_t p = off[t]; p < off[t + 1]; ++p) lpos[list[p]] = base[t] + (p - off[t]);
 }
 
+__global__ void k_slot_owner(const uint32_t* off, uint32_t lo, uint32_t hi, uint32_t* dst) {
+    for (uint32_t v = lo + blockIdx.x * blockDim.x + threadIdx.x; v < hi; v += gridDim.x * blockDim.x)
+        for (uint32_t s = off[v]; s < off[v + 1]; ++s) dst[s] = v;
+}
+
 __global__ void k_sort_segments(const uint32_t* off, uint32_t* vals, uint32_t n) {
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
         const uint32_t b = off[v], e = off[v + 1];
@@ -2151,6 +2158,10 @@ void launch_add_u32(uint32_t* x, const uint32_t* y, uint32_t n, const Launch& l)
 void launch_lpos_lists(const uint32_t* off, const uint32_t* list, uint32_t nt, const uint32_t* base, uint32_t* lpos,
                        const Launch& l) {
     hipLaunchKernelGGL(k_lpos_lists, dim3(l.grid), dim3(kBlock), 0, l.stream, off, list, nt, base, lpos);
+}
+
+void launch_slot_owner(const uint32_t* off, uint32_t lo, uint32_t hi, uint32_t* dst, const Launch& l) {
+    if (hi > lo) hipLaunchKernelGGL(k_slot_owner, dim3(l.grid), dim3(kBlock), 0, l.stream, off, lo, hi, dst);
 }
 
 void launch_sort_segments(const uint32_t* off, uint32_t* vals, uint32_t n, const Launch& l) {
