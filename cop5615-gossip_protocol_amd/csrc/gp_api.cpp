@@ -15,9 +15,7 @@
 #endif
 constexpr uint32_t kQuietMinActors = 1u << 20;
 // Full gossip done bitmap: one bit per actor, then its summary (one bit per 32-actor word).
-inline size_t dbits_words(size_t n) { return (n + 31) / 32; }
 constexpr uint32_t kDsumMinActors = 1u << 25;  // the summary is used from here (dbits > an L2)
-inline size_t dbits_alloc_words(size_t n) { return dbits_words(n) + (dbits_words(n) + 31) / 32; }
 // Full gossip on one GPU: the receipt tally (gp_kernels.h GsTally) is built from this many actors
 // and used in a round after one that emitted at least actors / kTallyThrDiv chains (scaled by
 // the share of nodes not done).  With the batched placement 8 rather than 2: C4 66.7 -> 61.6 ms,
@@ -177,7 +175,9 @@ struct Handle {
     uint32_t* cnt = nullptr;
     uint8_t* gstate = nullptr;
     uint32_t* inc[2] = {nullptr, nullptr};
-    uint32_t* dbits = nullptr;  // full gossip on one GPU: done bitmap (k_gs_full4's sender filter)
+    uint32_t* dbits = nullptr;  // full gossip: done bitmap (k_gs_full4's sender filter); a shard's is
+                                // biased (global bit = actor id) and covers its own actors
+    uint32_t* dsum = nullptr;   // its summary (one bit per all-done word), from kDsumMinActors actors
     GsTally tally{};            // full gossip on one GPU: receipt tally by target bucket (cnt null: off)
     // generic push-sum buckets
     uint32_t* bcnt[2] = {nullptr, nullptr};
@@ -292,7 +292,7 @@ struct Handle {
             a.act_cur = act[(r + 1u) & 1u];
         }
         a.dbits = dbits;
-        a.dsum = dbits && own() >= kDsumMinActors ? dbits + dbits_words(own()) : nullptr;
+        a.dsum = dsum;
         a.inc_prev = inc[p];
         a.inc_cur = inc[c];
         a.bcnt_prev = bcnt[p];
@@ -487,7 +487,14 @@ int reset(Handle* h) {
         if (h->generic) {
             HIP_TRY(hipMemsetAsync(h->inc[0] + lo, 0, n * sizeof(uint32_t), h->stream));
             HIP_TRY(hipMemsetAsync(h->inc[1] + lo, 0, n * sizeof(uint32_t), h->stream));
-            if (h->dbits) HIP_TRY(hipMemsetAsync(h->dbits, 0, dbits_alloc_words(n) * sizeof(uint32_t), h->stream));
+            if (h->dbits) {  // words lo >> 5 .. (hi - 1) >> 5, then the summary's
+                const size_t w0 = lo >> 5, nw = ((h->hi + 31u) >> 5) - w0;
+                HIP_TRY(hipMemsetAsync(h->dbits + w0, 0, nw * sizeof(uint32_t), h->stream));
+                if (h->dsum) {
+                    const size_t s0 = lo >> 10, ns = ((h->hi + 1023u) >> 10) - s0;
+                    HIP_TRY(hipMemsetAsync(h->dsum + s0, 0, ns * sizeof(uint32_t), h->stream));
+                }
+            }
             if (h->tally.cnt) {
                 HIP_TRY(hipMemsetAsync(h->tally.chains, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t),
                                        h->stream));
@@ -545,7 +552,7 @@ const char* round_kernel_name(const Handle* h) {
         return h->g.has_link ? (e ? "k_gs_pull<true, true>" : "k_gs_pull<true, false>")
                              : (e ? "k_gs_pull<false, true>" : "k_gs_pull<false, false>");
     }
-    if (h->gossip) return "k_gs_push";
+    if (h->gossip) return h->sharded ? "k_gs_full4x" : "k_gs_push";
     if (h->generic) return "k_ps_push_emit";
     if (h->sharded && h->g.has_link && h->rmsg[0]) return h->act[0] ? "k_ps_quiet<2>" : "k_ps_pull<2, false>";
     if (h->g.has_link) return h->act[0] ? "k_ps_quiet<1>" : "k_ps_pull<1, false>";
@@ -602,7 +609,7 @@ void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed) {
     const Launch l = h->L();
     if (h->gossip) {
         if (h->generic) {  // adds into inc_cur, consumed (zeroed) by F(k+1)
-            if (x) launch_gs_push_x(a, *x, l);
+            if (x) launch_gs_full4x(a, *x, l);
             else if (full_quad(h)) {
                 launch_gs_full4(a, h->tally, l);
                 launch_gs_tally(a, h->tally, l);
@@ -1378,7 +1385,15 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
         if ((rc = h->alloc(&h->cnt, n, lo)) || (rc = h->alloc(&h->gstate, n, lo))) return bail(rc);
         if (h->generic) {
             if ((rc = h->alloc(&h->inc[0], n, lo)) || (rc = h->alloc(&h->inc[1], n, lo))) return bail(rc);
-            if (full_quad(h) && (rc = h->alloc(&h->dbits, dbits_alloc_words(n)))) return bail(rc);
+            // done bitmap and summary of the own actors (global bit / word numbering)
+            if (full_quad(h) || h->sharded) {
+                const size_t w0 = lo >> 5, nw = ((h->hi + 31u) >> 5) - w0 + 1;
+                if ((rc = h->alloc(&h->dbits, nw, (int64_t)w0))) return bail(rc);
+                if (n >= kDsumMinActors) {
+                    const size_t s0 = lo >> 10, ns = ((h->hi + 1023u) >> 10) - s0 + 1;
+                    if ((rc = h->alloc(&h->dsum, ns, (int64_t)s0))) return bail(rc);
+                }
+            }
             const uint32_t nb = (uint32_t)((n + (1u << kTallyShift) - 1) >> kTallyShift);
             // the tally is a speed path: where its 128 KB of dynamic LDS cannot be allowed (another
             // ARCH), the handle keeps the receipt atomics, which give the same results

@@ -1279,7 +1279,10 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
                 atomicOr(x.overflow, 2u);
                 continue;
             }
-            if (full) atomicAdd(&a.inc_cur[t], 1u);
+            if (full) {  // a receipt for a done actor is dropped (program.fs:92; exact: the state after
+                         // F(applied), which F(applied + 1) filters with)
+                if (!(a.dbits && ((a.dbits[t >> 5] >> (t & 31u)) & 1u))) atomicAdd(&a.inc_cur[t], 1u);
+            }
             else if (gossip) a.lcnt_cur[t] = (uint8_t)((e >> 31) + 1u);
             else {  // the sender's message into the receiver's slot, the slot marked
                 a.rmsg_cur[t] = in.msg[i];
@@ -1551,6 +1554,120 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < t.nb; i += kBlock) t.cnt[i * t.W + blockIdx.x] = tcnt[i];
     }
+}
+
+// Full gossip on a shard of several ranks: k_gs_full4's walk over this rank's actors
+// [lo, hi), four consecutive actors per lane (the quads of the first and last lanes may hold other
+// ranks' actors, which are masked out: neither applied nor emitted).  A receipt for one of this
+// rank's actors takes the sender-side done filter of the one-GPU kernel on this rank's done bitmap
+// (global bit = actor id; its summary from 2^25 actors), then a memory-side atomic; a receipt for
+// another rank's actor becomes an entry of that rank's chunk (the target id), reserved per block and
+// peer.  The receiver drops the entries for its done actors before the atomic (k_shard_unpack): the
+// filter program.fs:92 applies there exactly, on the state after the round the sender ran.
+__global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
+    const uint32_t r = a.r;
+    unsigned long long prev = 0;
+    if (r) prev = gate_count(a, (long long)r - 1);
+    if (r && prev >= a.target) return;
+    const bool filter = (unsigned long long)GP_GS_FILTER_DIV * prev >= a.target;  // global count
+    const uint32_t lo = a.lo, hi = a.hi;
+    // quads from a multiple of 8 (8 lanes = 32 actors = one bitmap word)
+    const uint32_t q0 = (lo >> 2) & ~7u, q1 = (hi + 3u) >> 2, nq = q1 - q0;
+    const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;
+    uint32_t q, end, step;
+    node_range(q0, q1, span4, q, end, step);
+    uint32_t newly = 0;
+    // block-uniform trip count: block_reserve synchronises the block; lanes past the end idle
+    for (; q - threadIdx.x < end; q += step) {
+        const bool valid = q < end;
+        const uint32_t v0 = q << 2;
+        uint32_t st4 = 0, done4 = 0, mine = 0;  // mine: actors of this rank among v0 .. v0+3
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) mine |= (valid && v0 + j - lo < hi - lo) ? 1u << j : 0u;
+        if (mine) {
+            st4 = *reinterpret_cast<const uint32_t*>(a.gstate + v0);
+            uint4 in4 = make_uint4(0u, 0u, 0u, 0u);
+            if (r) in4 = *reinterpret_cast<const uint4*>(a.inc_prev + v0);
+            uint32_t inc[4] = {in4.x, in4.y, in4.z, in4.w};
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                if (!((mine >> j) & 1u)) inc[j] = 0u;  // another rank's actor (or padding)
+            if (inc[0] | inc[1] | inc[2] | inc[3]) {
+                *reinterpret_cast<uint4*>(a.inc_prev + v0) = make_uint4(0u, 0u, 0u, 0u);
+                uint4 c4 = *reinterpret_cast<const uint4*>(a.cnt + v0);
+                uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
+                const uint32_t st0 = st4;
+                bool counted = false;
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t st = (st4 >> (8u * j)) & 0xFFu;
+                    uint32_t tok = st & 3u, done = (st >> 2) & 1u;
+                    if (inc[j] && !done) {
+                        counted = true;
+                        const uint32_t c0 = c[j], c1 = c0 + inc[j];
+                        c[j] = c1;
+                        if (c0 == 0) ++tok;                              // program.fs:99-100
+                        if (c0 <= a.threshold && c1 > a.threshold) {     // program.fs:102-104
+                            done = 1;
+                            ++newly;
+                            done4 |= 1u << j;
+                        }
+                        st4 = (st4 & ~(0xFFu << (8u * j))) | ((tok | (done << 2)) << (8u * j));
+                    }
+                }
+                if (counted) *reinterpret_cast<uint4*>(a.cnt + v0) = make_uint4(c[0], c[1], c[2], c[3]);
+                if (st4 != st0) *reinterpret_cast<uint32_t*>(a.gstate + v0) = st4;
+            }
+        }
+        // emit round r: one draw per activation chain (program.fs:89-95); local receipts now, remote
+        // ones after the block's reservation
+        bool want[8];
+        uint32_t peer[8], tgt[8], pos[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t v = v0 + j, tok = ((mine >> j) & 1u) ? (st4 >> (8u * j)) & 3u : 0u;
+            uint32_t u[2] = {0u, 0u};
+            if (tok) {
+                const uint4 px = philox(v, r, kStreamGossip, a.seed);
+                const uint32_t t0 = scale_draw(px.x, a.nodes), t1 = scale_draw(px.y, a.nodes);
+                u[0] = t0 + (t0 >= v ? 1u : 0u);
+                u[1] = t1 + (t1 >= v ? 1u : 0u);
+            }
+#pragma unroll
+            for (uint32_t c = 0; c < 2; ++c) {
+                const bool send = tok > c;
+                const bool local = u[c] - lo < hi - lo;
+                want[2 * j + c] = send && !local;
+                tgt[2 * j + c] = u[c];
+                peer[2 * j + c] = want[2 * j + c] ? owner(x.abnd, x.world, u[c]) : 0u;
+                if (send && local) {
+                    uint32_t b = 0;
+                    if (filter && a.dsum && ((a.dsum[u[c] >> 10] >> ((u[c] >> 5) & 31u)) & 1u)) b = ~0u;
+                    else if (filter) b = a.dbits[u[c] >> 5];
+                    if (!((b >> (u[c] & 31u)) & 1u)) atomicAdd(&a.inc_cur[u[c]], 1u);
+                }
+            }
+        }
+        block_reserve(x, want, peer, pos);
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k)
+            if (want[k]) put<false>(x, peer[k], pos[k], tgt[k], make_double2(0.0, 0.0));
+        // the reports of this round into the done bitmap: 8 lanes = 32 actors = one word
+        uint32_t w = done4 << ((q & 7u) * 4u);
+        w |= __shfl_xor(w, 1, 64);
+        w |= __shfl_xor(w, 2, 64);
+        w |= __shfl_xor(w, 4, 64);
+        if (w && (q & 7u) == 0u) {
+            const uint32_t wi = q >> 3;
+            if (a.dsum) {
+                const uint32_t old = atomicOr(&a.dbits[wi], w);
+                if ((old | w) == ~0u && old != ~0u) atomicOr(&a.dsum[wi >> 5], 1u << (wi & 31u));
+            } else {
+                atomicOr(&a.dbits[wi], w);
+            }
+        }
+    }
+    if (r) block_add(newly, a.parts, (long long)r - 1);
 }
 
 // Tallied round: place every receipt of F(r) into its bucket's segment, at this workgroup's
@@ -2115,6 +2232,10 @@ void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l
 
 void launch_gs_push_x(const RoundArgs& a, const Xchg& x, const Launch& l) {
     hipLaunchKernelGGL(k_gs_push_x, dim3(l.grid), dim3(kBlock), 0, l.stream, a, x);
+}
+
+void launch_gs_full4x(const RoundArgs& a, const Xchg& x, const Launch& l) {
+    hipLaunchKernelGGL(k_gs_full4x, dim3(l.grid), dim3(kBlock), 0, l.stream, a, x);
 }
 
 void launch_shard_halo(const RoundArgs& a, const Xchg& x, int pushsum, hipStream_t s) {
