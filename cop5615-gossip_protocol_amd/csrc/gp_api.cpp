@@ -554,7 +554,7 @@ const char* round_kernel_name(const Handle* h) {
     }
     if (h->gossip) return h->sharded ? "k_gs_full4x" : "k_gs_push";
     if (h->generic) return "k_ps_push_emit";
-    if (h->sharded && h->g.has_link && h->rmsg[0]) return h->act[0] ? "k_ps_quiet<2>" : "k_ps_pull<2, false>";
+    if (h->sharded && h->g.has_link && h->rmsg[0]) return h->act[0] ? "k_ps_quiet_x" : "k_ps_pull<2, false>";
     if (h->g.has_link) return h->act[0] ? "k_ps_quiet<1>" : "k_ps_pull<1, false>";
     return h->act[0] ? "k_ps_quiet<0>" : "k_ps_pull<0, false>";
 }
@@ -621,7 +621,7 @@ void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed) {
     } else if (h->generic) {
         launch_ps_push_emit(a, l);
     } else {
-        launch_ps_pull(a, l);
+        launch_ps_pull(a, l, x);
     }
 }
 
@@ -631,7 +631,8 @@ int launch_aux(Handle* h, int64_t k, const Xchg* x) {
     const RoundArgs a = h->args(r);
     const Launch l = h->L();
     int rc;
-    if (!fused_marks(h) && (rc = clear_tags_if_due(h, r))) return rc;
+    // (a shard clears before its round kernel: its tail rounds write their own link marks)
+    if (!fused_marks(h) && !h->sharded && (rc = clear_tags_if_due(h, r))) return rc;
     if (h->gossip) {
         if (!h->generic && h->g.has_link) {
             if (x) launch_gs_link_scatter_x(a, *x, l);
@@ -677,7 +678,7 @@ int clear_act_if_due(Handle* h, int64_t k) {
 // Round k with its three timing events (slot i of the event ring).
 int launch_round(Handle* h, int64_t k, const Xchg* x, bool timing, int64_t i) {
     int rc;
-    if (fused_marks(h) && (rc = clear_tags_if_due(h, (uint32_t)k))) return rc;
+    if ((fused_marks(h) || h->sharded) && (rc = clear_tags_if_due(h, (uint32_t)k))) return rc;
     if ((rc = clear_act_if_due(h, k))) return rc;
     if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i], h->stream));
     launch_main(h, k, x, timing);

@@ -202,7 +202,7 @@ constexpr uint32_t kActShift = kActSeg == 64u ? 6u : kActSeg == 32u ? 5u : kActS
 static_assert((1u << kActShift) == kActSeg, "GP_ACT_SEG: 4, 8, 16, 32 or 64");
 
 // round kernels
-void launch_ps_pull(const RoundArgs& a, const Launch& l);
+void launch_ps_pull(const RoundArgs& a, const Launch& l, const Xchg* x = nullptr);  // x: a shard of several ranks
 void launch_gs_pull(const RoundArgs& a, const Launch& l);
 // Gossip grid rounds on graphs below 2^18 actors (one GPU) issue their level-1 loads ahead of
 // the gate: k_gs_pull<LINK, true>.  (At 1M actors the unconditional loads cost more than the

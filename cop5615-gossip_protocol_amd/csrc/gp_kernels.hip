@@ -164,6 +164,57 @@ __device__ __forceinline__ PsOut ps_update(uint8_t& f, double2 held, double ss, 
     return o;
 }
 
+// ------------------------------------------------------------------ shard exchange helpers
+// Lanes below this one whose bit is set in m.
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// Owner rank of x under the range bounds b[0..world] (world <= 16: a short uniform loop).
+__device__ __forceinline__ uint32_t owner(const uint32_t* b, uint32_t world, uint32_t x) {
+    uint32_t q = 0;
+    for (uint32_t i = 1; i < world; ++i) q += x >= b[i] ? 1u : 0u;
+    return q;
+}
+
+__device__ __forceinline__ uint32_t* ctr_at(const Xchg& x, uint32_t q, uint32_t sub) {
+    return x.pcount + (q * kSub + sub) * kCtrStride;
+}
+
+__device__ __forceinline__ uint32_t my_sub() { return blockIdx.x % kSub; }
+
+// Append (entry, msg) to peer q's chunk, sub-segment my_sub(), at pos, or flag the overflow (never
+// silently dropped: gp_shard_sync fails the run with GP_EOVERFLOW).
+template <bool MSG>
+__device__ __forceinline__ void put(const Xchg& x, uint32_t q, uint32_t pos, uint32_t entry, double2 m) {
+    const PeerOut& o = x.out[q];
+    if (pos < o.cap) {
+        const uint32_t i = my_sub() * o.cap + pos;
+        o.slot[i] = entry;
+        if (MSG) o.msg[i] = m;
+    } else {
+        atomicOr(x.overflow, 1u);
+    }
+}
+
+// Wave-level reservation for one entry per lane (lanes with want): one atomic per peer present on
+// the sub-segment counter of peer q (the quiet-tail rounds of a shard, where entries are few and the
+// walk is per wave).  Every lane of the wave must call it.
+__device__ __forceinline__ uint32_t wave_reserve(const Xchg& x, bool want, uint32_t q) {
+    uint32_t pos = 0;
+    uint64_t left = __ballot(want);
+    while (left) {  // wave-uniform: one peer per trip
+        const uint32_t lead = (uint32_t)__builtin_ctzll(left);
+        const uint32_t pq = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)lead);
+        const uint64_t m = __ballot(want && q == pq);
+        uint32_t base = 0;
+        if ((threadIdx.x & 63u) == lead) base = atomicAdd(ctr_at(x, pq, my_sub()), (uint32_t)__popcll(m));
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)lead);
+        if (want && q == pq) pos = base + mbcnt64(m);
+        left &= ~m;
+    }
+    return pos;
+}
+
 // ------------------------------------------------------------------ push-sum, grid topologies
 // Grid in-neighbour slots in ascending source order: v-P, v-G, v-1, v+1, v+G, v+P (presence
 // bits 4, 2, 0, 1, 3, 5); the sender in slot k targets v iff its direction code is the
@@ -281,10 +332,6 @@ __device__ __forceinline__ uint32_t ab(uint32_t i) {
     return (kAblate & BIT) ? (i & 0xFFFu) : i;
 }
 
-// Lanes below this one whose bit is set in m.
-__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
 // A/B knob: the message as one 16-byte non-temporal store (1) or two 8-byte ones (0).
 #ifndef GP_NT16
 #define GP_NT16 0
@@ -420,9 +467,16 @@ __device__ __forceinline__ PsLevel1 ps_level1(const RoundArgs& a, const Geom& g,
 
 // FF: message loads for the first kFiredLoads FIRED link slots only (one GPU; the shards' quiet
 // kernel, which spills with one load per unrolled slot) instead of one per unrolled slot.
+// A shard's quiet-tail round routes its own link messages (the scatter pass's work in the dense
+// rounds): ps_finish reports the message of an actor whose round-r message took its extra link.
+struct LinkSend {
+    bool fired = false;
+    double2 msg;
+};
+
 template <int LM, bool PRE = false, bool FF = (LM == 1 || kFiredShards)>
 __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
-                                              const PsLevel1& p, bool mark) {
+                                              const PsLevel1& p, bool mark, LinkSend* ls = nullptr) {
     const uint32_t m = p.m;
     if (!m) return 0;
     const uint32_t code = (kAblate & 8u) ? kth_bit(m, v % popc(m))
@@ -617,6 +671,10 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
     if constexpr (LM == 1 && kFuseLinkMarks) {  // the link pass's mark, written by the sender
         if (o.send && code == kDirLink) mark_store(a, &a.lcnt_cur[ab<262144u>(a.lpos[ab<4096u>(v)])], (uint8_t)a.tag_cur);
     }
+    if (LM == 2 && ls && o.send && code == kDirLink) {
+        ls->fired = true;
+        ls->msg = o.msg;
+    }
     if (f != f0) a.flags[v] = f;
     if (o.conv_now) a.frozen[v] = o.msg;
     if (mark) {  // the waves with work in round r + 1: v's own if it still updates, its target's
@@ -634,8 +692,8 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
 
 template <int LM, bool FF = (LM == 1 || kFiredShards)>
 __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
-                                             bool mark = false) {
-    return ps_finish<LM, false, FF>(a, g, r, v, ps_level1<LM>(a, g, r, v), mark);
+                                             bool mark = false, LinkSend* ls = nullptr) {
+    return ps_finish<LM, false, FF>(a, g, r, v, ps_level1<LM>(a, g, r, v), mark, ls);
 }
 
 // The quiet-wave tail with compaction.  Marks are per segment of kActSeg actors: F(r) marks the
@@ -740,7 +798,7 @@ __device__ __forceinline__ bool tail_next(const RoundArgs& a, TailWalk& t, uint8
 // its direction bytes become kDirNone and nothing else changes.
 // Q: quiet-wave marks allocated (a.act_cur != null); the small graphs run without (Q = false).
 template <int LM, bool Q>
-__device__ __forceinline__ void ps_pull_body(const RoundArgs& a) {
+__device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp = nullptr) {
     const Geom g = a.g;
     const uint32_t r = a.r;
     uint32_t newly = 0;
@@ -790,9 +848,24 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a) {
                 u = v;
                 v += step;
             }
+            LinkSend ls;
             if (u - a.lo < a.hi - a.lo) {  // lo <= u < hi (a shard's edge segments)
-                newly += ps_actor<LM, LM == 1 || LM == 2 || kFiredShards>(a, g, r, u, mark);
+                newly += ps_actor<LM, LM == 1 || LM == 2 || kFiredShards>(a, g, r, u, mark, LM == 2 ? &ls : nullptr);
                 ++walked;
+            }
+            if constexpr (LM == 2) {
+                // A shard's tail round routes its own link messages (k_ps_link_scatter_x skips these
+                // rounds): a slot of this rank gets its mark, another rank's an entry of its chunk,
+                // positions reserved per wave (the tail's entries are few).  Wave-uniform here.
+                if (tail) {
+                    const Xchg& x = *xp;
+                    const uint32_t lp = load_sel(a.lpos, ls.fired, u, a.lo);
+                    const bool remote = ls.fired && (lp < x.sbnd[x.rank] || lp >= x.sbnd[x.rank + 1]);
+                    if (ls.fired && !remote) a.lcnt_cur[lp] = (uint8_t)a.tag_cur;
+                    const uint32_t q = remote ? owner(x.sbnd, x.world, lp) : 0u;
+                    const uint32_t pos = wave_reserve(x, remote, q);
+                    if (remote) put<true>(x, q, pos, lp, ls.msg);
+                }
             }
         }
         block_add(newly, a.parts, r);
@@ -823,6 +896,12 @@ template <int LM>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PSQ_WAVES))) GP_PSQ_SGPR_ATTR void k_ps_quiet(
     RoundArgs a) {
     ps_pull_body<LM, true>(a);
+}
+// A shard of several ranks (LM 2): the same kernel with the exchange descriptor, so its tail rounds
+// route their own link messages.
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PSQ_WAVES))) GP_PSQ_SGPR_ATTR void k_ps_quiet_x(
+    RoundArgs a, Xchg x) {
+    ps_pull_body<2, true>(a, &x);
 }
 
 // ------------------------------------------------------------------ gossip, grid topologies
@@ -984,19 +1063,8 @@ __global__ __launch_bounds__(kBlock) void k_link_count(RoundArgs a) {
 }
 
 // ------------------------------------------------------------------ shard exchange
-// Owner rank of x under the range bounds b[0..world] (world <= 16: a short uniform loop).
-__device__ __forceinline__ uint32_t owner(const uint32_t* b, uint32_t world, uint32_t x) {
-    uint32_t q = 0;
-    for (uint32_t i = 1; i < world; ++i) q += x >= b[i] ? 1u : 0u;
-    return q;
-}
 
 
-__device__ __forceinline__ uint32_t* ctr_at(const Xchg& x, uint32_t q, uint32_t sub) {
-    return x.pcount + (q * kSub + sub) * kCtrStride;
-}
-
-__device__ __forceinline__ uint32_t my_sub() { return blockIdx.x % kSub; }
 
 // Positions of K entries per thread in their peers' chunks, reserved per BLOCK: LDS counters per
 // peer, then one global atomic per (block, peer) on the block's sub-segment counter.  At 8 ranks
@@ -1019,19 +1087,6 @@ __device__ __forceinline__ void block_reserve(const Xchg& x, const bool (&want)[
         if (want[j]) pos[j] += base[q[j]];
 }
 
-// Append (entry, msg) to peer q's chunk, sub-segment my_sub(), at pos, or flag the overflow (never
-// silently dropped: gp_shard_sync fails the run with GP_EOVERFLOW).
-template <bool MSG>
-__device__ __forceinline__ void put(const Xchg& x, uint32_t q, uint32_t pos, uint32_t entry, double2 m) {
-    const PeerOut& o = x.out[q];
-    if (pos < o.cap) {
-        const uint32_t i = my_sub() * o.cap + pos;
-        o.slot[i] = entry;
-        if (MSG) o.msg[i] = m;
-    } else {
-        atomicOr(x.overflow, 1u);
-    }
-}
 
 // Actors per thread of the sharded link passes (block-strided): more per block means fewer
 // block-level reservations (three barriers and one global atomic per peer each).
@@ -1044,16 +1099,10 @@ __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg 
     if (applied_converged(a)) return;  // block-uniform: F(r) was a no-op
     const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
     const uint32_t base = a.lo + blockIdx.x * kBlock * kShardPer + threadIdx.x;
-    // Quiet tail: F(r) walked only the segments marked link_tag(r) in act_prev, and every actor it
-    // did not walk sends nothing; a block whose kShardPer * kBlock actors lie in unmarked segments
-    // has no message to route (most blocks of the tail: 33 -> a few us per rank-round at 100M / 8).
-    if (a.act_prev && a.r >= 2u && a.total[a.r - 2u] >= a.act_thr) {
-        static_assert(kShardPer * kBlock / kActSeg == kBlock, "one segment mark per thread (+1)");
-        const uint32_t s0 = (base - threadIdx.x) >> kActShift;
-        bool any = a.act_prev[s0 + threadIdx.x] == (uint8_t)a.tag_cur;
-        if (threadIdx.x == 0) any = any || a.act_prev[s0 + kBlock] == (uint8_t)a.tag_cur;
-        if (!__syncthreads_or(any)) return;  // block-uniform
-    }
+    // Quiet-tail rounds (F(r) walked the marked segments only): the round kernel routed its own
+    // link messages (k_ps_quiet_x); this pass, latency-bound over every actor, would cost 33-40 us
+    // per rank-round at 100M / 8 for the few that moved.
+    if (a.act_prev && a.r >= 2u && a.total[a.r - 2u] >= a.act_thr) return;
     const uint32_t slo = x.sbnd[x.rank], shi = x.sbnd[x.rank + 1];
     bool l[kShardPer];
 #pragma unroll
@@ -2135,14 +2184,14 @@ uint32_t span_for(uint32_t n, int grid) {
 #endif
 static int quiet_grid(const Launch& l) { return l.grid < 256 * GP_PSQ_PER_CU ? l.grid : 256 * GP_PSQ_PER_CU; }
 
-void launch_ps_pull(const RoundArgs& a, const Launch& l) {
+void launch_ps_pull(const RoundArgs& a, const Launch& l, const Xchg* x) {
     const unsigned lds = GP_PS_LDS_CAP;
     const bool q = a.act_cur != nullptr;
     if (!a.g.has_link) {
         if (q) hipLaunchKernelGGL((k_ps_quiet<0>), dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a);
         else hipLaunchKernelGGL((k_ps_pull<0, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
     } else if (a.rmsg_prev) {  // a shard of several ranks
-        if (q) hipLaunchKernelGGL((k_ps_quiet<2>), dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a);
+        if (q) hipLaunchKernelGGL(k_ps_quiet_x, dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a, *x);
         else hipLaunchKernelGGL((k_ps_pull<2, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
     } else if (q) {
         hipLaunchKernelGGL((k_ps_quiet<1>), dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a);

@@ -15,7 +15,7 @@ loop() {  # name n topology algorithm round_kernel
 }
 for c in ${LOOPS:-ps gs}; do
   case $c in
-    ps) loop loop100m_ps 100000000 Imp3D push-sum "k_ps_quiet<2>" || exit 1 ;;
-    gs) loop loop100m_gs 100000000 full gossip "${GS_KERNEL:-k_gs_push_x}" || exit 1 ;;
+    ps) loop loop100m_ps 100000000 Imp3D push-sum "k_ps_quiet_x" || exit 1 ;;
+    gs) loop loop100m_gs 100000000 full gossip "${GS_KERNEL:-k_gs_full4x}" || exit 1 ;;
   esac
 done
