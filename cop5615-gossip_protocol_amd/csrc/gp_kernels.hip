@@ -733,22 +733,25 @@ static_assert(kQuadGrid >= 1 && kQuadGrid <= 4 && kQuadFired >= 1 && kQuadFired 
 // scratch by the selects that look a key up (LLVM rewrites the select chain as an indexed load).
 struct Pre4 {
     uint32_t b0 = ~0u, b1 = ~0u, b2 = ~0u, b3 = ~0u;
+    uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;  // the fired list: the source of each slot
     double2 m0, m1, m2, m3;
     template <uint32_t T>
-    __device__ __forceinline__ void set(uint32_t b, double2 m) {
-        if constexpr (T == 0) { b0 = b; m0 = m; }
-        else if constexpr (T == 1) { b1 = b; m1 = m; }
-        else if constexpr (T == 2) { b2 = b; m2 = m; }
-        else { b3 = b; m3 = m; }
+    __device__ __forceinline__ void set(uint32_t b, double2 m, uint32_t u = 0) {
+        if constexpr (T == 0) { b0 = b; m0 = m; u0 = u; }
+        else if constexpr (T == 1) { b1 = b; m1 = m; u1 = u; }
+        else if constexpr (T == 2) { b2 = b; m2 = m; u2 = u; }
+        else { b3 = b; m3 = m; u3 = u; }
     }
-    // the message of key b among the first K; found = false if absent
+    // the message (and source) of key b among the first K; found = false if absent
     template <uint32_t K>
-    __device__ __forceinline__ double2 get(uint32_t b, bool& found) const {
+    __device__ __forceinline__ double2 get(uint32_t b, bool& found, uint32_t* src = nullptr) const {
         double2 v = m0;
+        uint32_t u = u0;
         found = b0 == b;
-        if constexpr (K > 1) { if (b1 == b) v = m1; found = found || b1 == b; }
-        if constexpr (K > 2) { if (b2 == b) v = m2; found = found || b2 == b; }
-        if constexpr (K > 3) { if (b3 == b) v = m3; found = found || b3 == b; }
+        if constexpr (K > 1) { if (b1 == b) { v = m1; u = u1; } found = found || b1 == b; }
+        if constexpr (K > 2) { if (b2 == b) { v = m2; u = u2; } found = found || b2 == b; }
+        if constexpr (K > 3) { if (b3 == b) { v = m3; u = u3; } found = found || b3 == b; }
+        if (src) *src = u;
         return v;
     }
 };
@@ -762,10 +765,9 @@ __device__ __forceinline__ uint32_t ld_u32_any(const uint8_t* p) {  // byte-alig
 template <int LM>
 __device__ __forceinline__ void quad_actor(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v0, uint32_t j,
                                            const uint32_t (&m)[4], const uint32_t (&hits)[4], const double2 (&M)[4],
-                                           const uint32_t (&off)[5], uint32_t li0, const uint32_t (&S)[8], uint32_t& fl,
-                                           const Pre4& gp, const Pre4& fp,
-                                           const uint32_t (&lp4)[4], uint32_t F4, bool mark, uint32_t& newly,
-                                           uint32_t& codes, uint32_t& fout) {
+                                           const uint32_t (&off)[5], uint32_t li0, uint32_t& fl,
+                                           const Pre4& gp, const Pre4& fp, uint32_t F4, bool mark, uint32_t& newly,
+                                           uint32_t& codes, uint32_t& fout, uint32_t& lsend) {
         const uint32_t v = v0 + j;
         if (!m[j]) return;
         uint8_t f = (uint8_t)((F4 >> (8u * j)) & 0xFFu);
@@ -797,12 +799,13 @@ __device__ __forceinline__ void quad_actor(const RoundArgs& a, const Geom& g, ui
             const uint32_t rel_lo = off[j] - li0, rel_hi = off[j + 1] - li0;
             while (fl && (uint32_t)__builtin_ctz(fl) < rel_hi) {  // this actor's fired slots among the first 8
                 const uint32_t i = (uint32_t)__builtin_ctz(fl);
-                uint32_t u = S[0];
-#pragma unroll
-                for (uint32_t c = 1; c < 8; ++c) u = i == c ? S[c] : u;
                 bool found;
-                double2 val = fp.get<kQuadFired>(i, found);
-                if (!found) val = a.msg_prev[u];
+                uint32_t u;
+                double2 val = fp.get<kQuadFired>(i, found, &u);
+                if (!found) {  // rare: more than kQuadFired fired slots in the quad
+                    u = a.rev_src[li0 + i];
+                    val = a.msg_prev[u];
+                }
                 flush(u);
                 add(val);
                 fl &= fl - 1u;
@@ -824,9 +827,7 @@ __device__ __forceinline__ void quad_actor(const RoundArgs& a, const Geom& g, ui
             __builtin_nontemporal_store(o.msg.y, &a.msg_cur[v].y);
         }
         if (o.send) codes = (codes & ~(0xFFu << (8u * j))) | (code << (8u * j));
-        if constexpr (LM == 1 && kFuseLinkMarks) {
-            if (o.send && code == kDirLink) mark_store(a, &a.lcnt_cur[lp4[j]], (uint8_t)a.tag_cur);
-        }
+        if (o.send && code == kDirLink) lsend |= 1u << j;  // its link mark is stored after the quad
         if (f != f0) fout = (fout & ~(0xFFu << (8u * j))) | ((uint32_t)f << (8u * j));
         if (o.conv_now) {
             a.frozen[v] = o.msg;
@@ -915,7 +916,7 @@ __device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, u
         if constexpr (kQuadGrid > 2) one(std::integral_constant<uint32_t, 2>{});
         if constexpr (kQuadGrid > 3) one(std::integral_constant<uint32_t, 3>{});
     }
-    uint32_t S[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, fired = 0;
+    uint32_t S[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, fired = 0;  // live up to the level-3 loads
     if (LM != 0 && r) {
         typedef uint32_t u4v __attribute__((ext_vector_type(4)));
         u4v s0, s1;
@@ -940,7 +941,7 @@ __device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, u
             uint32_t u = S[0];
 #pragma unroll
             for (uint32_t c = 1; c < 8; ++c) u = i == c ? S[c] : u;
-            fp.set<decltype(T)::value>(i, load_sel(a.msg_prev, rest != 0u, u, a.lo));
+            fp.set<decltype(T)::value>(i, load_sel(a.msg_prev, rest != 0u, u, a.lo), u);
             rest &= rest - 1u;
         };
         one(std::integral_constant<uint32_t, 0>{});
@@ -951,18 +952,23 @@ __device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, u
     // ---- collect (canonical order), update and emit, actor by actor
     uint32_t newly = 0, codes = 0, fout = F4;
     uint32_t fl = fired;  // fired slots < 8 not consumed yet (CSR order = actor, then source)
-    uint32_t lp4[4] = {0u, 0u, 0u, 0u};
-    if constexpr (LM == 1 && kFuseLinkMarks) {
-        const uint4 l4 = *reinterpret_cast<const uint4*>(a.lpos + v0);
-        lp4[0] = l4.x; lp4[1] = l4.y; lp4[2] = l4.z; lp4[3] = l4.w;
-    }
+    uint32_t lsend = 0;   // actors whose message took the extra link
     codes = 0x07070707u;  // kDirNone for every actor that sends nothing (or has no neighbour)
     static_assert(kDirNone == 7, "kDirNone bytes");
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) quad_actor<LM>(a, g, r, v0, j, m, hits, M, off, li0, S, fl, gp, fp, lp4, F4,
-                                                     mark, newly, codes, fout);
+    for (uint32_t j = 0; j < 4; ++j)
+        quad_actor<LM>(a, g, r, v0, j, m, hits, M, off, li0, fl, gp, fp, F4, mark, newly, codes, fout, lsend);
     __builtin_nontemporal_store(codes, reinterpret_cast<uint32_t*>(a.dir_cur + v0));
     if (fout != F4) *reinterpret_cast<uint32_t*>(a.flags + v0) = fout;
+    if constexpr (LM == 1 && kFuseLinkMarks) {  // the link marks of the quad's link messages (one lpos load)
+        if (lsend) {
+            const uint4 l4 = *reinterpret_cast<const uint4*>(a.lpos + v0);
+            if (lsend & 1u) mark_store(a, &a.lcnt_cur[l4.x], (uint8_t)a.tag_cur);
+            if (lsend & 2u) mark_store(a, &a.lcnt_cur[l4.y], (uint8_t)a.tag_cur);
+            if (lsend & 4u) mark_store(a, &a.lcnt_cur[l4.z], (uint8_t)a.tag_cur);
+            if (lsend & 8u) mark_store(a, &a.lcnt_cur[l4.w], (uint8_t)a.tag_cur);
+        }
+    }
     return newly;
 }
 
