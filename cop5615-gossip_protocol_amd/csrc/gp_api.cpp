@@ -24,6 +24,11 @@ constexpr size_t kTallyMinActors = 1u << 20;
 #ifndef GP_DENSE4
 #define GP_DENSE4 1
 #endif
+// Small Imp3D push-sum graphs on one GPU (no quiet marks): link senders also write their message into
+// the receiver's CSR slot (k_ps_pull<3>; A/B knob)
+#ifndef GP_SLOT_MSGS
+#define GP_SLOT_MSGS 1
+#endif
 #ifndef GP_TALLY_THR_DIV
 #define GP_TALLY_THR_DIV 8
 #endif
@@ -393,8 +398,10 @@ int build_links(Handle* h) {
     if (!h->generic) {  // pull kernels
         // per-slot link marks of the own slots (gossip chains, push-sum round tags)
         if ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))) return rc;
-        // a remote sender's link message lands in the receiver's slot, read in CSR order (k_ps_pull<2>)
-        if (h->sharded && h->world > 1 && !h->gossip &&
+        // a remote sender's link message lands in the receiver's slot, read in CSR order (k_ps_pull<2>);
+        // on a small one-GPU graph every link message does (k_ps_pull<3>, the latency-bound rounds)
+        const bool slot_msgs = (h->sharded && h->world > 1) || (!h->sharded && !h->act[0] && GP_SLOT_MSGS);
+        if (slot_msgs && !h->gossip &&
             ((rc = h->alloc(&h->rmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->rmsg[1], (size_t)nsl, slo))))
             return rc;
         // the unpack marks the segment of a remote link message's receiver (quiet tail)
@@ -560,6 +567,7 @@ const char* round_kernel_name(const Handle* h) {
     if (h->gossip) return h->sharded ? "k_gs_full4x" : "k_gs_push";
     if (h->generic) return "k_ps_push_emit";
     if (h->sharded && h->g.has_link && h->rmsg[0]) return h->act[0] ? "k_ps_quiet_x" : "k_ps_pull<2, false>";
+    if (h->g.has_link && h->rmsg[0]) return "k_ps_pull<3, false>";
     if (h->dense4) return h->g.has_link ? "k_ps_dense4<1>+k_ps_quiet<1>" : "k_ps_dense4<0>+k_ps_quiet<0>";
     if (h->g.has_link) return h->act[0] ? "k_ps_quiet<1>" : "k_ps_pull<1, false>";
     return h->act[0] ? "k_ps_quiet<0>" : "k_ps_pull<0, false>";

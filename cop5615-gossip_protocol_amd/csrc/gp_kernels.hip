@@ -412,7 +412,10 @@ __device__ __forceinline__ void mark_store(const RoundArgs& a, uint8_t* p, uint8
 // CSR slot of the first kLinkUnroll, the source id and link count (coalesced: CSR order);
 // (3) the messages of the links that fired.
 // LM: 0 no extra links; 1 links; 2 links on a shard of several ranks: a sender outside [lo, hi)
-// is remote, and the exchange wrote its message into the receiver's slot, rmsg_prev[slot].
+// is remote, and the exchange wrote its message into the receiver's slot, rmsg_prev[slot]; 3 links
+// on a small one-GPU graph: every link sender writes its message into the receiver's slot
+// (rmsg_cur[lpos[v]]) as well as its own row, so the receiver loads the slot messages together
+// with the slot sources and marks (one dependent load level less: the round is latency-bound).
 
 // Level 1 of one actor's loads (own flags, the six neighbours' direction bytes, the CSR range),
 // split out so the small-graph kernel can issue them before its gate resolves.  PRE (small
@@ -631,7 +634,10 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
             } else {
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) {
-                    if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
+                    if constexpr (LM == 3) {  // the slot holds the message: its address needs only li,
+                                              // so the load goes out with the sources and marks
+                        lm[k] = load_sel(a.rmsg_prev, k < nl, li + k, a.slot_lo);
+                    } else if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
                         lm[k] = a.rmsg_prev[li + k];
                     } else {
                         lm[k] = ((kAblate & 524288u) && k >= 2u)
@@ -650,7 +656,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                 if (a.lcnt_prev[li + k] == a.tag_prev) {
                     const uint32_t u = a.rev_src[li + k];
                     flush(u);
-                    add(LM == 2 && (u < a.lo || u >= a.hi) ? a.rmsg_prev[li + k] : a.msg_prev[u]);
+                    add(LM == 3 || (LM == 2 && (u < a.lo || u >= a.hi)) ? a.rmsg_prev[li + k] : a.msg_prev[u]);
                 }
             }
         }
@@ -672,6 +678,13 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
     __builtin_nontemporal_store(o.send ? (uint8_t)code : kDirNone, &a.dir_cur[v]);
     if constexpr (LM == 1 && kFuseLinkMarks) {  // the link pass's mark, written by the sender
         if (o.send && code == kDirLink) mark_store(a, &a.lcnt_cur[ab<262144u>(a.lpos[ab<4096u>(v)])], (uint8_t)a.tag_cur);
+    }
+    if constexpr (LM == 3) {  // small graphs: the message into the receiver's slot too, and its mark
+        if (o.send && code == kDirLink) {
+            const uint32_t lp = a.lpos[v];
+            a.rmsg_cur[lp] = o.msg;
+            a.lcnt_cur[lp] = (uint8_t)a.tag_cur;
+        }
     }
     if (LM == 2 && ls && o.send && code == kDirLink) {
         ls->fired = true;
@@ -2488,6 +2501,8 @@ void launch_ps_pull(const RoundArgs& a, const Launch& l, const Xchg* x) {
     if (!a.g.has_link) {
         if (q) hipLaunchKernelGGL((k_ps_quiet<0>), dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a);
         else hipLaunchKernelGGL((k_ps_pull<0, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
+    } else if (a.rmsg_prev && !a.sharded) {  // one GPU, small graph: link messages by slot
+        hipLaunchKernelGGL((k_ps_pull<3, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
     } else if (a.rmsg_prev) {  // a shard of several ranks
         if (q) hipLaunchKernelGGL(k_ps_quiet_x, dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a, *x);
         else hipLaunchKernelGGL((k_ps_pull<2, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
