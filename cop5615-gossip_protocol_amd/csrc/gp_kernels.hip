@@ -870,9 +870,12 @@ __device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, u
     if (r) {
         // ---- level 1
         const uint32_t Do = *reinterpret_cast<const uint32_t*>(a.dir_prev + v0);
-        const uint32_t Dm1 = a.dir_prev[v0 - 1u], Dp4 = a.dir_prev[v0 + 4u];
-        const uint32_t DmP = ld_u32_any(a.dir_prev + (v0 - g.plane)), DmG = ld_u32_any(a.dir_prev + (v0 - g.gx));
-        const uint32_t DpG = ld_u32_any(a.dir_prev + (v0 + g.gx)), DpP = ld_u32_any(a.dir_prev + (v0 + g.plane));
+        // signed offsets: below the first plane they reach into the arrays' padding (a plane + 8
+        // bytes on each side), never wrap around
+        const int64_t iv = (int64_t)v0;
+        const uint32_t Dm1 = a.dir_prev[iv - 1], Dp4 = a.dir_prev[iv + 4];
+        const uint32_t DmP = ld_u32_any(a.dir_prev + (iv - (int64_t)g.plane)), DmG = ld_u32_any(a.dir_prev + (iv - (int64_t)g.gx));
+        const uint32_t DpG = ld_u32_any(a.dir_prev + (iv + (int64_t)g.gx)), DpP = ld_u32_any(a.dir_prev + (iv + (int64_t)g.plane));
         if constexpr (LM != 0) {
             const uint4 o4 = *reinterpret_cast<const uint4*>(a.rev_off + v0);
             off[0] = o4.x;
