@@ -244,7 +244,7 @@ def test_quiet_waves_default_and_reset():
         assert gs.converged and (gs.round, gs.completed) == (cs.round, cs.completed)
         np.testing.assert_array_equal(gpu.read_trace(), cpu.read_trace())
         check_same(gpu, cpu, "push-sum")
-        assert gpu.kernel_stats()["kernel"] == "k_ps_quiet<1>"
+        assert gpu.kernel_stats()["kernel"] == "k_ps_dense4<1>+k_ps_quiet<1>"  # dense rounds, then the tail
         gpu.reset()
     gpu.close()
     cpu.close()
