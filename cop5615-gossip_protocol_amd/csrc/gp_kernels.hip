@@ -736,7 +736,7 @@ __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, 
 #define GP_QUAD_FIRED 2
 #endif
 #ifndef GP_PS4_WAVES
-#define GP_PS4_WAVES 4
+#define GP_PS4_WAVES 3
 #endif
 constexpr uint32_t kQuadGrid = GP_QUAD_GRID;
 constexpr uint32_t kQuadFired = GP_QUAD_FIRED;
@@ -780,7 +780,8 @@ __device__ __forceinline__ void quad_actor(const RoundArgs& a, const Geom& g, ui
                                            const uint32_t (&m)[4], const uint32_t (&hits)[4], const double2 (&M)[4],
                                            const uint32_t (&off)[5], uint32_t li0, uint32_t& fl,
                                            const Pre4& gp, const Pre4& fp, uint32_t F4, bool mark, uint32_t& newly,
-                                           uint32_t& codes, uint32_t& fout, uint32_t& lsend) {
+                                           uint32_t& codes, uint32_t& fout, uint32_t& lsend, double2& out) {
+        // (out is the lane's LDS slot of row v: its old value, M[j], was read before)
         const uint32_t v = v0 + j;
         if (!m[j]) return;
         uint8_t f = (uint8_t)((F4 >> (8u * j)) & 0xFFu);
@@ -835,10 +836,8 @@ __device__ __forceinline__ void quad_actor(const RoundArgs& a, const Geom& g, ui
         const uint32_t code = kth_bit(m[j], scale_draw(philox_x(v, r, kStreamPush, a.seed), popc(m[j])));
         const uint8_t f0 = f;
         const PsOut o = ps_update(f, M[j], ss, ww, cin, a.delta, a.term_limit);
-        if (o.send) {
-            __builtin_nontemporal_store(o.msg.x, &a.msg_cur[v].x);
-            __builtin_nontemporal_store(o.msg.y, &a.msg_cur[v].y);
-        }
+        out = o.msg;  // into the wave's LDS rows, stored with the others (a row that sends nothing
+                      // is never read)
         if (o.send) codes = (codes & ~(0xFFu << (8u * j))) | (code << (8u * j));
         if (o.send && code == kDirLink) lsend |= 1u << j;  // its link mark is stored after the quad
         if (f != f0) fout = (fout & ~(0xFFu << (8u * j))) | ((uint32_t)f << (8u * j));
@@ -855,14 +854,16 @@ __device__ __forceinline__ void quad_actor(const RoundArgs& a, const Geom& g, ui
         }
     }
 
+// q: this lane's quad (valid: inside its span); rows_end: the end of the wave's actors (the span's
+// end, hi at most), beyond which no row is loaded or stored.
 template <int LM>
-__device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t q, bool mark,
-                                            uint32_t& walked) {
+__device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t q, bool valid,
+                                            uint32_t rows_end, bool mark, uint32_t& walked, double2* xr) {
     const uint32_t v0 = q << 2;
     uint32_t m[4];
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) m[j] = presence(g, v0 + j);  // 0: isolated actor / padding
-    walked += (v0 + 4u <= a.hi) ? 4u : (v0 < a.hi ? a.hi - v0 : 0u);
+    for (uint32_t j = 0; j < 4; ++j) m[j] = valid ? presence(g, v0 + j) : 0u;  // 0: isolated actor / padding
+    if (valid) walked += (v0 + 4u <= a.hi) ? 4u : (v0 < a.hi ? a.hi - v0 : 0u);
     const uint32_t F4 = *reinterpret_cast<const uint32_t*>(a.flags + v0);
     uint32_t hits[4] = {0u, 0u, 0u, 0u};  // grid hits per actor, slot bits 0..5 (ascending source)
     uint32_t li0 = 0, off[5] = {0u, 0u, 0u, 0u, 0u}, nl = 0;
@@ -908,9 +909,27 @@ __device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, u
             hits[j] = (kAblate & 16u) ? 0u : h;
         }
     }
-    // ---- level 2: own rows (held / in-quad +-1 messages), outside grid hits, CSR sources and marks
+    // ---- level 2: own rows (held / in-quad +-1 messages), outside grid hits, CSR sources and marks.
+    // The wave's 256 rows are loaded coalesced (instruction i, lane l: row 64 i + l of the wave) and
+    // handed to the lanes that own them through LDS (row k at (k % 4) * 64 + k / 4: conflict-free
+    // 16-byte writes and reads); loading its quad's rows directly, a lane strides 64 bytes and every
+    // instruction touches four times the lines (the first cut ran 2x slower).
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wrow0 = (q - lane) << 2;  // first actor of the wave's 256 (quads q - lane .. q - lane + 63)
+    if (r) {
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) M[j] = r ? a.msg_prev[v0 + j] : make_double2((double)(v0 + j), 1.0);
+        for (uint32_t i = 0; i < 4; ++i) {
+            const uint32_t k = 64u * i + lane;
+            xr[(k & 3u) * 64u + (k >> 2)] = load_sel(a.msg_prev, wrow0 + k < rows_end, wrow0 + k, a.lo);
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) M[j] = xr[j * 64u + lane];
+        __builtin_amdgcn_wave_barrier();
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) M[j] = make_double2((double)(v0 + j), 1.0);
+    }
     // grid hits whose message is not one of M[]: +-G, +-G^2 always, -1 of actor 0, +1 of actor 3
     uint32_t ext = 0;
 #pragma unroll
@@ -932,14 +951,26 @@ __device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, u
         if constexpr (kQuadGrid > 2) one(std::integral_constant<uint32_t, 2>{});
         if constexpr (kQuadGrid > 3) one(std::integral_constant<uint32_t, 3>{});
     }
-    uint32_t S[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, fired = 0;  // live up to the level-3 loads
+    // the sources of the first 8 slots (live up to the level-3 loads), picked for a fired mask by a
+    // priority chain on its bits: as an array indexed by slot number (or a vector with a dynamic
+    // element), LLVM put them in scratch and read them back behind a vmcnt(0) wait
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    u4v s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
+    uint32_t fired = 0;
+    auto lowest_src = [&](uint32_t mask) {  // the source of the lowest slot set in mask (0: s0.x)
+        uint32_t u = s1.w;
+        u = (mask & 64u) ? s1.z : u;
+        u = (mask & 32u) ? s1.y : u;
+        u = (mask & 16u) ? s1.x : u;
+        u = (mask & 8u) ? s0.w : u;
+        u = (mask & 4u) ? s0.z : u;
+        u = (mask & 2u) ? s0.y : u;
+        u = (mask & 1u) ? s0.x : u;
+        return u;
+    };
     if (LM != 0 && r) {
-        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-        u4v s0, s1;
         __builtin_memcpy(&s0, &a.rev_src[li0], sizeof s0);
         __builtin_memcpy(&s1, &a.rev_src[li0 + 4u], sizeof s1);
-        S[0] = s0.x; S[1] = s0.y; S[2] = s0.z; S[3] = s0.w;
-        S[4] = s1.x; S[5] = s1.y; S[6] = s1.z; S[7] = s1.w;
         const uint32_t* mw = reinterpret_cast<const uint32_t*>(a.lcnt_prev + (li0 & ~3u));
         const uint32_t w0 = mw[0], w1 = mw[1], w2 = mw[2];
         const uint32_t sh = 8u * (li0 & 3u);
@@ -954,9 +985,7 @@ __device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, u
         uint32_t rest = fired;
         auto one = [&](auto T) {
             const uint32_t i = (uint32_t)__builtin_ctz(rest | 0x100u);  // 8: none
-            uint32_t u = S[0];
-#pragma unroll
-            for (uint32_t c = 1; c < 8; ++c) u = i == c ? S[c] : u;
+            const uint32_t u = lowest_src(rest);
             fp.set<decltype(T)::value>(i, load_sel(a.msg_prev, rest != 0u, u, a.lo), u);
             rest &= rest - 1u;
         };
@@ -973,7 +1002,21 @@ __device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, u
     static_assert(kDirNone == 7, "kDirNone bytes");
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j)
-        quad_actor<LM>(a, g, r, v0, j, m, hits, M, off, li0, fl, gp, fp, F4, mark, newly, codes, fout, lsend);
+        quad_actor<LM>(a, g, r, v0, j, m, hits, M, off, li0, fl, gp, fp, F4, mark, newly, codes, fout, lsend,
+                       xr[j * 64u + lane]);
+    // the wave's new rows, stored coalesced (non-temporal: read next round only), rows of lanes
+    // past the end of the span excepted
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+        const uint32_t k = 64u * i + lane;
+        const double2 o = xr[(k & 3u) * 64u + (k >> 2)];
+        if (wrow0 + k < rows_end) {
+            __builtin_nontemporal_store(o.x, &a.msg_cur[wrow0 + k].x);
+            __builtin_nontemporal_store(o.y, &a.msg_cur[wrow0 + k].y);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
     __builtin_nontemporal_store(codes, reinterpret_cast<uint32_t*>(a.dir_cur + v0));
     if (fout != F4) *reinterpret_cast<uint32_t*>(a.flags + v0) = fout;
     if constexpr (LM == 1 && kFuseLinkMarks) {  // the link marks of the quad's link messages (one lpos load)
@@ -1000,7 +1043,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS4_W
     const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;
     uint32_t q, end, step, newly = 0, walked = 0;
     node_range(0u, nq, span4, q, end, step);
-    for (; q < end; q += step) newly += ps_quad<LM>(a, g, r, q, mark, walked);
+    __shared__ double2 xrow[kBlock / 64u][256];  // per wave: its 256 message rows (4 KB)
+    double2* xr = xrow[threadIdx.x >> 6];
+    // wave-uniform trip count (the rows go through LDS per wave); a lane past the end takes the
+    // padding quad at end (its actors are >= hi: no presence, nothing stored)
+    for (; q - (threadIdx.x & 63u) < end; q += step) {
+        const uint32_t rows_end = (end << 2) < a.hi ? end << 2 : a.hi;
+        newly += ps_quad<LM>(a, g, r, q, q < end, rows_end, mark, walked, xr);
+    }
     block_add(newly, a.parts, r);
     if (a.work) block_add_u64(walked, a.work + (blockIdx.x & (kParts - 1)) * kWorkStride);
 }
