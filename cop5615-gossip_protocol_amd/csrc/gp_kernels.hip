@@ -859,7 +859,11 @@ __device__ __forceinline__ void quad_actor(const RoundArgs& a, const Geom& g, ui
 template <int LM>
 __device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t q, bool valid,
                                             uint32_t rows_end, bool mark, uint32_t& walked, double2* xr) {
-    const uint32_t v0 = q << 2;
+    // a lane past the end of the span reads the wave's first quad (valid memory) and computes and
+    // stores nothing: its own quad may lie past the arrays (the span's end is hi) or in another span
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wq0 = q - lane;
+    const uint32_t v0 = (valid ? q : wq0) << 2;
     uint32_t m[4];
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) m[j] = valid ? presence(g, v0 + j) : 0u;  // 0: isolated actor / padding
@@ -914,8 +918,7 @@ __device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, u
     // handed to the lanes that own them through LDS (row k at (k % 4) * 64 + k / 4: conflict-free
     // 16-byte writes and reads); loading its quad's rows directly, a lane strides 64 bytes and every
     // instruction touches four times the lines (the first cut ran 2x slower).
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wrow0 = (q - lane) << 2;  // first actor of the wave's 256 (quads q - lane .. q - lane + 63)
+    const uint32_t wrow0 = wq0 << 2;  // first actor of the wave's 256 (quads wq0 .. wq0 + 63)
     if (r) {
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i) {
@@ -1017,8 +1020,8 @@ __device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, u
         }
     }
     __builtin_amdgcn_wave_barrier();
-    __builtin_nontemporal_store(codes, reinterpret_cast<uint32_t*>(a.dir_cur + v0));
-    if (fout != F4) *reinterpret_cast<uint32_t*>(a.flags + v0) = fout;
+    if (valid) __builtin_nontemporal_store(codes, reinterpret_cast<uint32_t*>(a.dir_cur + v0));
+    if (fout != F4) *reinterpret_cast<uint32_t*>(a.flags + v0) = fout;  // (never for an invalid lane)
     if constexpr (LM == 1 && kFuseLinkMarks) {  // the link marks of the quad's link messages (one lpos load)
         if (lsend) {
             const uint4 l4 = *reinterpret_cast<const uint4*>(a.lpos + v0);
