@@ -21,9 +21,6 @@ constexpr uint32_t kDsumMinActors = 1u << 25;  // the summary is used from here 
 // the share of nodes not done).  With the batched placement 8 rather than 2: C4 66.7 -> 61.6 ms,
 // 10M +2% (profiles/round3/c4_scatter/cli_tally_thr.txt).
 constexpr size_t kTallyMinActors = 1u << 20;
-#ifndef GP_DENSE4
-#define GP_DENSE4 1
-#endif
 // Small Imp3D push-sum graphs on one GPU (no quiet marks): link senders also write their message into
 // the receiver's CSR slot (k_ps_pull<3>; A/B knob)
 #ifndef GP_SLOT_MSGS
@@ -179,8 +176,6 @@ struct Handle {
     double2* frozen = nullptr;
     uint8_t* act[2] = {nullptr, nullptr};  // quiet-wave marks, one byte per 64 actors (ping-pong)
     uint32_t act_thr = 0;
-    bool dense4 = false;      // one GPU, 3D / Imp3D push-sum with quiet marks: k_ps_dense4 is available
-    bool dense4_now = false;  // this batch runs k_ps_dense4 (the host saw fewer than act_thr converged)
     // gossip
     uint32_t* cnt = nullptr;
     uint8_t* gstate = nullptr;
@@ -236,8 +231,8 @@ struct Handle {
     // bytes on both sides: the row loads of the first and last lanes (v0 - 2 .. v0 + 5, a lane's
     // 16 link marks) read a few elements past [first, first + count) and never use them.
     template <class T>
-    int alloc(T** p, size_t count, int64_t first = 0, size_t extra_pad = 0) {
-        const size_t kPad = 256 + extra_pad * sizeof(T);  // extra_pad: elements readable on both sides
+    int alloc(T** p, size_t count, int64_t first = 0) {
+        constexpr size_t kPad = 256;
         const int64_t f0 = first & ~(int64_t)15;
         const size_t n = (size_t)(first - f0) + count;
         void* q = nullptr;
@@ -568,7 +563,6 @@ const char* round_kernel_name(const Handle* h) {
     if (h->generic) return "k_ps_push_emit";
     if (h->sharded && h->g.has_link && h->rmsg[0]) return h->act[0] ? "k_ps_quiet_x" : "k_ps_pull<2, false>";
     if (h->g.has_link && h->rmsg[0]) return "k_ps_pull<3, false>";
-    if (h->dense4) return h->g.has_link ? "k_ps_dense4<1>+k_ps_quiet<1>" : "k_ps_dense4<0>+k_ps_quiet<0>";
     if (h->g.has_link) return h->act[0] ? "k_ps_quiet<1>" : "k_ps_pull<1, false>";
     return h->act[0] ? "k_ps_quiet<0>" : "k_ps_pull<0, false>";
 }
@@ -634,8 +628,6 @@ void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed) {
         }
     } else if (h->generic) {
         launch_ps_push_emit(a, l);
-    } else if (h->dense4_now) {
-        launch_ps_dense4(a, l);
     } else {
         launch_ps_pull(a, l, x);
     }
@@ -741,13 +733,7 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
     const int64_t goal = h->rounds + max_rounds;
     int rc;
     while (!h->converged && h->rounds < goal) {
-        // Dense rounds run four actors per lane (k_ps_dense4) until the host has seen act_thr nodes
-        // converged, then the quiet kernel; either kernel computes every round exactly, the switch is
-        // a speed choice.  Near the switch batches are short, so few tail rounds run the dense kernel.
-        h->dense4_now = h->dense4 && (uint64_t)h->completed < h->act_thr;
-        int64_t cap_b = h->batch;
-        if (h->dense4_now && h->completed * 100 >= h->lay.nodes * 90) cap_b = std::min<int64_t>(cap_b, 16);
-        const int64_t B = std::min<int64_t>(cap_b, goal - h->rounds);
+        const int64_t B = std::min<int64_t>(h->batch, goal - h->rounds);
         const int64_t before = h->completed;
         const bool was_tail = kTailBatch > 0 && before * 32 >= h->lay.nodes * 31;
         if ((rc = ensure_trace(h, h->next_kernel + B + 4))) return rc;
@@ -1450,10 +1436,6 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
             if (hipMemsetAsync(h->work, 0, (size_t)kParts * kWorkStride * sizeof *h->work, h->stream) != hipSuccess)
                 return bail(fail(GP_EHIP, "hipMemsetAsync failed"));
             h->act_thr = (uint32_t)((uint64_t)h->lay.nodes * GP_ACT_PCT / 100u);
-            // four actors per lane in the dense rounds (one GPU, z-planes: the +-G^2 direction dwords
-            // read the padded arrays); GP_DENSE4=0 in the environment: the quiet kernel in every round
-            const char* d4 = std::getenv("GP_DENSE4");
-            h->dense4 = GP_DENSE4 && !h->sharded && g.gz > 1 && !(d4 && d4[0] == '0');
         }
         if (h->generic) {  // single-GPU only: whole graph
             for (int i = 0; i < 2; ++i)
@@ -1463,11 +1445,8 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
             if ((rc = h->alloc(&h->tgt, A)) || (rc = h->alloc(&h->pos, A)) ||
                 (rc = h->alloc(&h->scan_scratch, scan_scratch_words((uint32_t)A))))
                 return bail(rc);
-        } else {
-            // the dense-round kernel (k_ps_dense4) loads the direction bytes of the +-1, +-G and +-G^2
-            // neighbours of four actors as whole dwords, unconditionally: a plane (+ 8) of padding
-            const size_t pad = h->dense4 ? (size_t)g.plane + 8u : 0u;
-            if ((rc = h->alloc(&h->dir[0], xn, xlo, pad)) || (rc = h->alloc(&h->dir[1], xn, xlo, pad))) return bail(rc);
+        } else if ((rc = h->alloc(&h->dir[0], xn, xlo)) || (rc = h->alloc(&h->dir[1], xn, xlo))) {
+            return bail(rc);
         }
     }
     if (g.has_link && (rc = build_links(h))) return bail(rc);

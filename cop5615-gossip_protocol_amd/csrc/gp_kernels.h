@@ -203,8 +203,6 @@ static_assert((1u << kActShift) == kActSeg, "GP_ACT_SEG: 4, 8, 16, 32 or 64");
 
 // round kernels
 void launch_ps_pull(const RoundArgs& a, const Launch& l, const Xchg* x = nullptr);  // x: a shard of several ranks
-// The dense rounds of a large graph on one GPU (lo = 0, 3D / Imp3D): four actors per lane.
-void launch_ps_dense4(const RoundArgs& a, const Launch& l);
 void launch_gs_pull(const RoundArgs& a, const Launch& l);
 // Gossip grid rounds on graphs below 2^18 actors (one GPU) issue their level-1 loads ahead of
 // the gate: k_gs_pull<LINK, true>.  (At 1M actors the unconditional loads cost more than the

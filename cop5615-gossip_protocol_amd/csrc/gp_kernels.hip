@@ -16,8 +16,6 @@
 // only; correctness never depends on it).
 #include "gp_kernels.h"
 
-#include <type_traits>
-
 namespace gp {
 
 namespace {
@@ -709,353 +707,6 @@ template <int LM, bool FF = (LM == 1 || kFiredShards)>
 __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
                                              bool mark = false, LinkSend* ls = nullptr) {
     return ps_finish<LM, false, FF>(a, g, r, v, ps_level1<LM>(a, g, r, v), mark, ls);
-}
-
-// ------------------------------------------------------------------ push-sum dense rounds, 4 actors per lane
-// The all-sending rounds of a large graph are bound per vector-memory instruction, not by HBM bytes
-// (round 3: TA / TD 80-90% busy), and one actor per lane spends ~17 load instructions
-// per actor, most of them on bytes (flags, six direction bytes) or on predicated 16-byte loads for
-// hits that rarely exist.  Here a lane takes four consecutive actors v0 .. v0+3 (v0 = 4q):
-//   * level 1: the four flags as one dword; the direction bytes of the +-G and +-G^2 neighbours as
-//     one (byte-aligned) dword each, the four own bytes (the +-1 neighbours inside the quad) as one
-//     aligned dword and the two outside it as bytes; the CSR offsets v0 .. v0+4 as 16 + 4 bytes;
-//   * level 2: the four own message rows (the held (S,W) of an actor that has not converged, and
-//     the +-1 messages inside the quad), the messages of the first kQuadGrid grid hits from outside
-//     the quad, the CSR sources of the quad's first 8 link slots (two 16-byte loads) and their marks
-//     (three dwords);
-//   * level 3: the messages of the first kQuadFired fired link slots.
-// Rarer cases (more hits, more slots) load on demand.  The collect of every actor is the canonical
-// ascending-source sum of ps_finish (grid hits merged with the CSR-ordered link sources), so the
-// results are identical.  Used in the rounds before the quiet tail (one GPU, from 2^20 actors; the
-// host switches to k_ps_quiet once the nodes it has seen converged reach act_thr); it also writes the
-// quiet-tail marks when the round it runs calls for them, so any round may run either kernel.
-#ifndef GP_QUAD_GRID
-#define GP_QUAD_GRID 3
-#endif
-#ifndef GP_QUAD_FIRED
-#define GP_QUAD_FIRED 2
-#endif
-#ifndef GP_PS4_WAVES
-#define GP_PS4_WAVES 3
-#endif
-constexpr uint32_t kQuadGrid = GP_QUAD_GRID;
-constexpr uint32_t kQuadFired = GP_QUAD_FIRED;
-static_assert(kQuadGrid >= 1 && kQuadGrid <= 4 && kQuadFired >= 1 && kQuadFired <= 4, "GP_QUAD_*: 1 .. 4");
-
-// Up to four preloaded (key, message) pairs in named registers: an array here would be turned into
-// scratch by the selects that look a key up (LLVM rewrites the select chain as an indexed load).
-struct Pre4 {
-    uint32_t b0 = ~0u, b1 = ~0u, b2 = ~0u, b3 = ~0u;
-    uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;  // the fired list: the source of each slot
-    double2 m0, m1, m2, m3;
-    template <uint32_t T>
-    __device__ __forceinline__ void set(uint32_t b, double2 m, uint32_t u = 0) {
-        if constexpr (T == 0) { b0 = b; m0 = m; u0 = u; }
-        else if constexpr (T == 1) { b1 = b; m1 = m; u1 = u; }
-        else if constexpr (T == 2) { b2 = b; m2 = m; u2 = u; }
-        else { b3 = b; m3 = m; u3 = u; }
-    }
-    // the message (and source) of key b among the first K; found = false if absent
-    template <uint32_t K>
-    __device__ __forceinline__ double2 get(uint32_t b, bool& found, uint32_t* src = nullptr) const {
-        double2 v = m0;
-        uint32_t u = u0;
-        found = b0 == b;
-        if constexpr (K > 1) { if (b1 == b) { v = m1; u = u1; } found = found || b1 == b; }
-        if constexpr (K > 2) { if (b2 == b) { v = m2; u = u2; } found = found || b2 == b; }
-        if constexpr (K > 3) { if (b3 == b) { v = m3; u = u3; } found = found || b3 == b; }
-        if (src) *src = u;
-        return v;
-    }
-};
-
-__device__ __forceinline__ uint32_t ld_u32_any(const uint8_t* p) {  // byte-aligned dword (gfx950 serves it)
-    return *reinterpret_cast<const uint32_t*>(p);
-}
-
-// One actor (j of the quad at v0) of ps_quad: collect, update, emit.  A separate inlined function
-// with a compile-time-unrolled caller, so every array stays in registers.
-template <int LM>
-__device__ __forceinline__ void quad_actor(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v0, uint32_t j,
-                                           const uint32_t (&m)[4], const uint32_t (&hits)[4], const double2 (&M)[4],
-                                           const uint32_t (&off)[5], uint32_t li0, uint32_t& fl,
-                                           const Pre4& gp, const Pre4& fp, uint32_t F4, bool mark, uint32_t& newly,
-                                           uint32_t& codes, uint32_t& fout, uint32_t& lsend, double2& out) {
-        // (out is the lane's LDS slot of row v: its old value, M[j], was read before)
-        const uint32_t v = v0 + j;
-        if (!m[j]) return;
-        uint8_t f = (uint8_t)((F4 >> (8u * j)) & 0xFFu);
-        double ss = 0.0, ww = 0.0;
-        uint32_t cin = 0;
-        auto add = [&](double2 mm) {
-            ss += mm.x;
-            ww += mm.y;
-            ++cin;
-        };
-        uint32_t pend = hits[j];
-        auto grid_val = [&](uint32_t k) -> double2 {
-            if (k == 2 && j > 0) return M[j - 1];
-            if (k == 3 && j < 3) return M[j + 1];
-            bool found;
-            double2 val = gp.get<kQuadGrid>(8u * j + k, found);
-            if (!found) val = a.msg_prev[slot_src(g, v, k)];  // rare: more than kQuadGrid outside hits
-            return val;
-        };
-        auto flush = [&](uint32_t bound) {
-#pragma unroll
-            for (uint32_t k = 0; k < 6; ++k)
-                if (((pend >> k) & 1u) && slot_src(g, v, k) < bound) {
-                    add(grid_val(k));
-                    pend &= ~(1u << k);
-                }
-        };
-        if (LM != 0 && r) {
-            const uint32_t rel_lo = off[j] - li0, rel_hi = off[j + 1] - li0;
-            while (fl && (uint32_t)__builtin_ctz(fl) < rel_hi) {  // this actor's fired slots among the first 8
-                const uint32_t i = (uint32_t)__builtin_ctz(fl);
-                bool found;
-                uint32_t u;
-                double2 val = fp.get<kQuadFired>(i, found, &u);
-                if (!found) {  // rare: more than kQuadFired fired slots in the quad
-                    u = a.rev_src[li0 + i];
-                    val = a.msg_prev[u];
-                }
-                flush(u);
-                add(val);
-                fl &= fl - 1u;
-            }
-            for (uint32_t i = rel_lo > 8u ? rel_lo : 8u; i < rel_hi; ++i) {  // rare: slots past the first 8
-                if (a.lcnt_prev[li0 + i] == (uint8_t)a.tag_prev) {
-                    const uint32_t u = a.rev_src[li0 + i];
-                    flush(u);
-                    add(a.msg_prev[u]);
-                }
-            }
-        }
-        flush(0xFFFFFFFFu);
-        const uint32_t code = kth_bit(m[j], scale_draw(philox_x(v, r, kStreamPush, a.seed), popc(m[j])));
-        const uint8_t f0 = f;
-        const PsOut o = ps_update(f, M[j], ss, ww, cin, a.delta, a.term_limit);
-        out = o.msg;  // into the wave's LDS rows, stored with the others (a row that sends nothing
-                      // is never read)
-        if (o.send) codes = (codes & ~(0xFFu << (8u * j))) | (code << (8u * j));
-        if (o.send && code == kDirLink) lsend |= 1u << j;  // its link mark is stored after the quad
-        if (f != f0) fout = (fout & ~(0xFFu << (8u * j))) | ((uint32_t)f << (8u * j));
-        if (o.conv_now) {
-            a.frozen[v] = o.msg;
-            ++newly;
-        }
-        if (mark) {  // quiet-tail marks for round r + 1 (ps_finish)
-            const uint8_t t = (uint8_t)link_tag(r + 1u);
-            if (!(f & 16u)) byte_store<GP_ACT_POL>(&a.act_cur[v >> kActShift], t);
-            if (o.send)
-                byte_store<GP_ACT_POL>(
-                    &a.act_cur[dir_target(g, v, code, code == kDirLink ? link_of(a.seed, v, a.nodes) : 0u) >> kActShift], t);
-        }
-    }
-
-// q: this lane's quad (valid: inside its span); rows_end: the end of the wave's actors (the span's
-// end, hi at most), beyond which no row is loaded or stored.
-template <int LM>
-__device__ __forceinline__ uint32_t ps_quad(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t q, bool valid,
-                                            uint32_t rows_end, bool mark, uint32_t& walked, double2* xr) {
-    // a lane past the end of the span reads the wave's first quad (valid memory) and computes and
-    // stores nothing: its own quad may lie past the arrays (the span's end is hi) or in another span
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wq0 = q - lane;
-    const uint32_t v0 = (valid ? q : wq0) << 2;
-    uint32_t m[4];
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) m[j] = valid ? presence(g, v0 + j) : 0u;  // 0: isolated actor / padding
-    if (valid) walked += (v0 + 4u <= a.hi) ? 4u : (v0 < a.hi ? a.hi - v0 : 0u);
-    const uint32_t F4 = *reinterpret_cast<const uint32_t*>(a.flags + v0);
-    uint32_t hits[4] = {0u, 0u, 0u, 0u};  // grid hits per actor, slot bits 0..5 (ascending source)
-    uint32_t li0 = 0, off[5] = {0u, 0u, 0u, 0u, 0u}, nl = 0;
-    double2 M[4];
-    if (r) {
-        // ---- level 1
-        const uint32_t Do = *reinterpret_cast<const uint32_t*>(a.dir_prev + v0);
-        // signed offsets: below the first plane they reach into the arrays' padding (a plane + 8
-        // bytes on each side), never wrap around
-        const int64_t iv = (int64_t)v0;
-        const uint32_t Dm1 = a.dir_prev[iv - 1], Dp4 = a.dir_prev[iv + 4];
-        const uint32_t DmP = ld_u32_any(a.dir_prev + (iv - (int64_t)g.plane)), DmG = ld_u32_any(a.dir_prev + (iv - (int64_t)g.gx));
-        const uint32_t DpG = ld_u32_any(a.dir_prev + (iv + (int64_t)g.gx)), DpP = ld_u32_any(a.dir_prev + (iv + (int64_t)g.plane));
-        if constexpr (LM != 0) {
-            const uint4 o4 = *reinterpret_cast<const uint4*>(a.rev_off + v0);
-            off[0] = o4.x;
-            off[1] = o4.y;
-            off[2] = o4.z;
-            off[3] = o4.w;
-            off[4] = a.rev_off[v0 + 4u];
-            if (v0 + 4u > a.hi) {  // the last quad: offsets past rev_off[hi] are padding (garbage), and
-                                   // a garbage slot count would read garbage sources
-                const uint32_t e = a.rev_off[a.hi];
-#pragma unroll
-                for (uint32_t j = 1; j < 5; ++j)
-                    if (v0 + j > a.hi) off[j] = e;
-            }
-            li0 = off[0];
-            nl = off[4] - off[0];
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            const uint32_t sh = 8u * j;
-            const uint32_t dm1 = j == 0 ? Dm1 : (Do >> (sh - 8u)) & 0xFFu;
-            const uint32_t dp1 = j == 3 ? Dp4 : (Do >> (sh + 8u)) & 0xFFu;
-            uint32_t h = 0;
-            h |= ((m[j] & 16u) && ((DmP >> sh) & 0xFFu) == 5u) ? 1u : 0u;   // v - G^2 sent +z
-            h |= ((m[j] & 4u) && ((DmG >> sh) & 0xFFu) == 3u) ? 2u : 0u;    // v - G sent +y
-            h |= ((m[j] & 1u) && dm1 == 1u) ? 4u : 0u;                      // v - 1 sent +x
-            h |= ((m[j] & 2u) && dp1 == 0u) ? 8u : 0u;                      // v + 1 sent -x
-            h |= ((m[j] & 8u) && ((DpG >> sh) & 0xFFu) == 2u) ? 16u : 0u;   // v + G sent -y
-            h |= ((m[j] & 32u) && ((DpP >> sh) & 0xFFu) == 4u) ? 32u : 0u;  // v + G^2 sent -z
-            hits[j] = (kAblate & 16u) ? 0u : h;
-        }
-    }
-    // ---- level 2: own rows (held / in-quad +-1 messages), outside grid hits, CSR sources and marks.
-    // The wave's 256 rows are loaded coalesced (instruction i, lane l: row 64 i + l of the wave) and
-    // handed to the lanes that own them through LDS (row k at (k % 4) * 64 + k / 4: conflict-free
-    // 16-byte writes and reads); loading its quad's rows directly, a lane strides 64 bytes and every
-    // instruction touches four times the lines (the first cut ran 2x slower).
-    const uint32_t wrow0 = wq0 << 2;  // first actor of the wave's 256 (quads wq0 .. wq0 + 63)
-    if (r) {
-#pragma unroll
-        for (uint32_t i = 0; i < 4; ++i) {
-            const uint32_t k = 64u * i + lane;
-            xr[(k & 3u) * 64u + (k >> 2)] = load_sel(a.msg_prev, wrow0 + k < rows_end, wrow0 + k, a.lo);
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) M[j] = xr[j * 64u + lane];
-        __builtin_amdgcn_wave_barrier();
-    } else {
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) M[j] = make_double2((double)(v0 + j), 1.0);
-    }
-    // grid hits whose message is not one of M[]: +-G, +-G^2 always, -1 of actor 0, +1 of actor 3
-    uint32_t ext = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t own = (j > 0 ? 4u : 0u) | (j < 3 ? 8u : 0u);
-        ext |= (hits[j] & ~own) << (8u * j);
-    }
-    Pre4 gp, fp;
-    {
-        uint32_t rest = ext;
-        auto one = [&](auto T) {
-            const uint32_t b = (uint32_t)__builtin_ctz(rest | 0x80000000u);  // 31: none
-            const uint32_t j = b >> 3, k = b & 7u;
-            gp.set<decltype(T)::value>(b, load_sel(a.msg_prev, rest != 0u, slot_src(g, v0 + j, k), a.lo));
-            rest &= rest - 1u;
-        };
-        one(std::integral_constant<uint32_t, 0>{});
-        if constexpr (kQuadGrid > 1) one(std::integral_constant<uint32_t, 1>{});
-        if constexpr (kQuadGrid > 2) one(std::integral_constant<uint32_t, 2>{});
-        if constexpr (kQuadGrid > 3) one(std::integral_constant<uint32_t, 3>{});
-    }
-    // the sources of the first 8 slots (live up to the level-3 loads), picked for a fired mask by a
-    // priority chain on its bits: as an array indexed by slot number (or a vector with a dynamic
-    // element), LLVM put them in scratch and read them back behind a vmcnt(0) wait
-    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-    u4v s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
-    uint32_t fired = 0;
-    auto lowest_src = [&](uint32_t mask) {  // the source of the lowest slot set in mask (0: s0.x)
-        uint32_t u = s1.w;
-        u = (mask & 64u) ? s1.z : u;
-        u = (mask & 32u) ? s1.y : u;
-        u = (mask & 16u) ? s1.x : u;
-        u = (mask & 8u) ? s0.w : u;
-        u = (mask & 4u) ? s0.z : u;
-        u = (mask & 2u) ? s0.y : u;
-        u = (mask & 1u) ? s0.x : u;
-        return u;
-    };
-    if (LM != 0 && r) {
-        __builtin_memcpy(&s0, &a.rev_src[li0], sizeof s0);
-        __builtin_memcpy(&s1, &a.rev_src[li0 + 4u], sizeof s1);
-        const uint32_t* mw = reinterpret_cast<const uint32_t*>(a.lcnt_prev + (li0 & ~3u));
-        const uint32_t w0 = mw[0], w1 = mw[1], w2 = mw[2];
-        const uint32_t sh = 8u * (li0 & 3u);
-        const uint64_t lo8 = (uint64_t)w0 | ((uint64_t)w1 << 32);
-        const uint64_t m8 = (lo8 >> sh) | (sh ? ((uint64_t)w2 << (64u - sh)) : 0ull);  // marks of li0 .. li0+7
-#pragma unroll
-        for (uint32_t i = 0; i < 8; ++i)
-            fired |= (i < nl && (uint8_t)(m8 >> (8u * i)) == (uint8_t)a.tag_prev) ? 1u << i : 0u;
-    }
-    // ---- level 3: the messages of the first kQuadFired fired slots
-    {
-        uint32_t rest = fired;
-        auto one = [&](auto T) {
-            const uint32_t i = (uint32_t)__builtin_ctz(rest | 0x100u);  // 8: none
-            const uint32_t u = lowest_src(rest);
-            fp.set<decltype(T)::value>(i, load_sel(a.msg_prev, rest != 0u, u, a.lo), u);
-            rest &= rest - 1u;
-        };
-        one(std::integral_constant<uint32_t, 0>{});
-        if constexpr (kQuadFired > 1) one(std::integral_constant<uint32_t, 1>{});
-        if constexpr (kQuadFired > 2) one(std::integral_constant<uint32_t, 2>{});
-        if constexpr (kQuadFired > 3) one(std::integral_constant<uint32_t, 3>{});
-    }
-    // ---- collect (canonical order), update and emit, actor by actor
-    uint32_t newly = 0, codes = 0, fout = F4;
-    uint32_t fl = fired;  // fired slots < 8 not consumed yet (CSR order = actor, then source)
-    uint32_t lsend = 0;   // actors whose message took the extra link
-    codes = 0x07070707u;  // kDirNone for every actor that sends nothing (or has no neighbour)
-    static_assert(kDirNone == 7, "kDirNone bytes");
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j)
-        quad_actor<LM>(a, g, r, v0, j, m, hits, M, off, li0, fl, gp, fp, F4, mark, newly, codes, fout, lsend,
-                       xr[j * 64u + lane]);
-    // the wave's new rows, stored coalesced (non-temporal: read next round only), rows of lanes
-    // past the end of the span excepted
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) {
-        const uint32_t k = 64u * i + lane;
-        const double2 o = xr[(k & 3u) * 64u + (k >> 2)];
-        if (wrow0 + k < rows_end) {
-            __builtin_nontemporal_store(o.x, &a.msg_cur[wrow0 + k].x);
-            __builtin_nontemporal_store(o.y, &a.msg_cur[wrow0 + k].y);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (valid) __builtin_nontemporal_store(codes, reinterpret_cast<uint32_t*>(a.dir_cur + v0));
-    if (fout != F4) *reinterpret_cast<uint32_t*>(a.flags + v0) = fout;  // (never for an invalid lane)
-    if constexpr (LM == 1 && kFuseLinkMarks) {  // the link marks of the quad's link messages (one lpos load)
-        if (lsend) {
-            const uint4 l4 = *reinterpret_cast<const uint4*>(a.lpos + v0);
-            if (lsend & 1u) mark_store(a, &a.lcnt_cur[l4.x], (uint8_t)a.tag_cur);
-            if (lsend & 2u) mark_store(a, &a.lcnt_cur[l4.y], (uint8_t)a.tag_cur);
-            if (lsend & 4u) mark_store(a, &a.lcnt_cur[l4.z], (uint8_t)a.tag_cur);
-            if (lsend & 8u) mark_store(a, &a.lcnt_cur[l4.w], (uint8_t)a.tag_cur);
-        }
-    }
-    return newly;
-}
-
-// One GPU (lo = 0): the quads of [0, hi) over the XCD-aware mapping of k_ps_pull.
-template <int LM>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PS4_WAVES))) void k_ps_dense4(RoundArgs a) {
-    const Geom g = a.g;
-    const uint32_t r = a.r;
-    const unsigned long long prev = gate_count(a, r);
-    if (prev >= a.target) return;
-    const bool mark = a.act_cur != nullptr && prev >= a.act_thr;
-    const uint32_t nq = (a.hi + 3u) >> 2;
-    const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;
-    uint32_t q, end, step, newly = 0, walked = 0;
-    node_range(0u, nq, span4, q, end, step);
-    __shared__ double2 xrow[kBlock / 64u][256];  // per wave: its 256 message rows (4 KB)
-    double2* xr = xrow[threadIdx.x >> 6];
-    // wave-uniform trip count (the rows go through LDS per wave); a lane past the end takes the
-    // padding quad at end (its actors are >= hi: no presence, nothing stored)
-    for (; q - (threadIdx.x & 63u) < end; q += step) {
-        const uint32_t rows_end = (end << 2) < a.hi ? end << 2 : a.hi;
-        newly += ps_quad<LM>(a, g, r, q, q < end, rows_end, mark, walked, xr);
-    }
-    block_add(newly, a.parts, r);
-    if (a.work) block_add_u64(walked, a.work + (blockIdx.x & (kParts - 1)) * kWorkStride);
 }
 
 // The quiet-wave tail with compaction.  Marks are per segment of kActSeg actors: F(r) marks the
@@ -2545,11 +2196,6 @@ uint32_t span_for(uint32_t n, int grid) {
 #define GP_PSQ_PER_CU 7
 #endif
 static int quiet_grid(const Launch& l) { return l.grid < 256 * GP_PSQ_PER_CU ? l.grid : 256 * GP_PSQ_PER_CU; }
-
-void launch_ps_dense4(const RoundArgs& a, const Launch& l) {
-    if (a.g.has_link) hipLaunchKernelGGL((k_ps_dense4<1>), dim3(l.grid), dim3(kBlock), 0, l.stream, a);
-    else hipLaunchKernelGGL((k_ps_dense4<0>), dim3(l.grid), dim3(kBlock), 0, l.stream, a);
-}
 
 void launch_ps_pull(const RoundArgs& a, const Launch& l, const Xchg* x) {
     const unsigned lds = GP_PS_LDS_CAP;
