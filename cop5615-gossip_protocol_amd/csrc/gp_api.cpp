@@ -881,10 +881,16 @@ Chunk chunk_layout(const Handle* h, int p, int q) {
         }
     }
     double mean = 0.0, exact = 0.0;
-    if (h->full) {  // every chain of p draws a target uniform over the other actors
-        const double chains = 2.0 * (double)size_p, share = (double)(h->abnd[q + 1] - h->abnd[q]) / (double)h->lay.nodes;
-        mean = chains * share;
-        exact = chains;
+    if (h->full) {
+        // every chain of p draws a target uniform over the other actors.  k_gs_full4x picks a
+        // sub-segment per 1024-actor chunk of p's range (chunk index mod kSub), so a sub-segment sees
+        // the chains of ceil(chunks / kSub) chunks at most: entry_cap_sub gets kSub times that
+        const int64_t q0 = (h->abnd[p] >> 2) & ~7LL, q1 = (h->abnd[p + 1] + 3) >> 2;
+        const int64_t chunks = ((q1 - 1) >> 8) - (q0 >> 8) + 1, per_sub = (chunks + kSub - 1) / kSub;
+        const double share = (double)(h->abnd[q + 1] - h->abnd[q]) / (double)h->lay.nodes;
+        const double chains = 2.0 * (double)std::min<int64_t>(size_p, per_sub * 1024);
+        mean = (double)kSub * chains * share;
+        exact = chains;  // one sub-segment's bound
     } else if (h->g.has_link) {
         for (int d = 1; d < 8; ++d) {
             const double n = (double)h->lhist[((size_t)p * h->world + q) * 8 + d];

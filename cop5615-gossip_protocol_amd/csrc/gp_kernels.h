@@ -237,7 +237,6 @@ int prepare_gs_tally();  // once per process: allow the tally pass's 128 KB of d
 // sharded variants: remote link / full-topology messages go to the send chunks of x
 void launch_ps_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);
 void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);
-void launch_gs_push_x(const RoundArgs& a, const Xchg& x, const Launch& l);
 void launch_gs_full4x(const RoundArgs& a, const Xchg& x, const Launch& l);  // full gossip, shards
 // halo faces of F(k) into the send chunks of rank +-1: direction bytes, crossing push-sum messages
 void launch_shard_halo(const RoundArgs& a, const Xchg& x, int pushsum, hipStream_t s);

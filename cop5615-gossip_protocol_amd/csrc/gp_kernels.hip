@@ -185,10 +185,11 @@ __device__ __forceinline__ uint32_t my_sub() { return blockIdx.x % kSub; }
 // Append (entry, msg) to peer q's chunk, sub-segment my_sub(), at pos, or flag the overflow (never
 // silently dropped: gp_shard_sync fails the run with GP_EOVERFLOW).
 template <bool MSG>
-__device__ __forceinline__ void put(const Xchg& x, uint32_t q, uint32_t pos, uint32_t entry, double2 m) {
+__device__ __forceinline__ void put(const Xchg& x, uint32_t q, uint32_t pos, uint32_t entry, double2 m,
+                                    uint32_t sub = kSub) {
     const PeerOut& o = x.out[q];
     if (pos < o.cap) {
-        const uint32_t i = my_sub() * o.cap + pos;
+        const uint32_t i = (sub < kSub ? sub : my_sub()) * o.cap + pos;
         o.slot[i] = entry;
         if (MSG) o.msg[i] = m;
     } else {
@@ -1085,7 +1086,8 @@ __global__ __launch_bounds__(kBlock) void k_link_count(RoundArgs a) {
 // per round (8 loopback shards of 80M actors).  Every thread of the block must call it.
 template <uint32_t K>
 __device__ __forceinline__ void block_reserve(const Xchg& x, const bool (&want)[K], const uint32_t (&q)[K],
-                                              uint32_t (&pos)[K]) {
+                                              uint32_t (&pos)[K], uint32_t sub = kSub) {
+    if (sub >= kSub) sub = my_sub();
     __shared__ uint32_t cnt[kMaxWorld], base[kMaxWorld];
     if (threadIdx.x < kMaxWorld) cnt[threadIdx.x] = 0u;
     __syncthreads();
@@ -1093,7 +1095,7 @@ __device__ __forceinline__ void block_reserve(const Xchg& x, const bool (&want)[
     for (uint32_t j = 0; j < K; ++j) pos[j] = want[j] ? atomicAdd(&cnt[q[j]], 1u) : 0u;
     __syncthreads();
     if (threadIdx.x < x.world && cnt[threadIdx.x])
-        base[threadIdx.x] = atomicAdd(ctr_at(x, threadIdx.x, my_sub()), cnt[threadIdx.x]);
+        base[threadIdx.x] = atomicAdd(ctr_at(x, threadIdx.x, sub), cnt[threadIdx.x]);
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < K; ++j)
@@ -1472,7 +1474,6 @@ __device__ __forceinline__ void gs_push_body(const RoundArgs& a, const Xchg* xp)
 
 __global__ __launch_bounds__(kBlock) void k_gs_push(RoundArgs a) { gs_push_body<false>(a, nullptr); }
 
-__global__ __launch_bounds__(kBlock) void k_gs_push_x(RoundArgs a, Xchg x) { gs_push_body<true>(a, &x); }
 
 // Full-topology gossip on one GPU (program.fs:89-105, "full" neighbours program.fs:201-206):
 // four consecutive actors per lane, so the per-actor streams (state byte, receipt and count
@@ -1710,10 +1711,14 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
                 }
             }
         }
-        block_reserve(x, want, peer, pos);
+        // sub-segment by the block-iteration's 1024-actor chunk (its first quad / 256, block-uniform):
+        // consecutive chunks of the range cycle through the kSub sub-segments whatever the grid, so
+        // gp_api.cpp sizes a sub-segment for ceil(chunks / kSub) chunks
+        const uint32_t sub = ((q - threadIdx.x) >> 8) % kSub;
+        block_reserve(x, want, peer, pos, sub);
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k)
-            if (want[k]) put<false>(x, peer[k], pos[k], tgt[k], make_double2(0.0, 0.0));
+            if (want[k]) put<false>(x, peer[k], pos[k], tgt[k], make_double2(0.0, 0.0), sub);
         // the reports of this round into the done bitmap: 8 lanes = 32 actors = one word
         uint32_t w = done4 << ((q & 7u) * 4u);
         w |= __shfl_xor(w, 1, 64);
@@ -2292,10 +2297,6 @@ void launch_ps_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l
 
 void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l) {
     if (const unsigned b = scatter_blocks(a)) hipLaunchKernelGGL(k_gs_link_scatter_x, dim3(b), dim3(kBlock), 0, l.stream, a, x);
-}
-
-void launch_gs_push_x(const RoundArgs& a, const Xchg& x, const Launch& l) {
-    hipLaunchKernelGGL(k_gs_push_x, dim3(l.grid), dim3(kBlock), 0, l.stream, a, x);
 }
 
 void launch_gs_full4x(const RoundArgs& a, const Xchg& x, const Launch& l) {
