@@ -26,6 +26,7 @@ constexpr size_t kTallyMinActors = 1u << 20;
 #ifndef GP_SLOT_MSGS
 #define GP_SLOT_MSGS 1
 #endif
+constexpr uint32_t kSlotMsgMaxActors = 1u << 18;
 #ifndef GP_TALLY_THR_DIV
 #define GP_TALLY_THR_DIV 8
 #endif
@@ -395,7 +396,10 @@ int build_links(Handle* h) {
         if ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))) return rc;
         // a remote sender's link message lands in the receiver's slot, read in CSR order (k_ps_pull<2>);
         // on a small one-GPU graph every link message does (k_ps_pull<3>, the latency-bound rounds)
-        const bool slot_msgs = (h->sharded && h->world > 1) || (!h->sharded && !h->act[0] && GP_SLOT_MSGS);
+        // (one GPU: up to 2^18 actors; at 1M actors the scattered 16-byte slot stores cost more than
+        // the load level they save, profiles/round4/small_imp3d)
+        const bool slot_msgs = (h->sharded && h->world > 1) ||
+                               (!h->sharded && !h->act[0] && GP_SLOT_MSGS && h->g.actors < kSlotMsgMaxActors);
         if (slot_msgs && !h->gossip &&
             ((rc = h->alloc(&h->rmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->rmsg[1], (size_t)nsl, slo))))
             return rc;
