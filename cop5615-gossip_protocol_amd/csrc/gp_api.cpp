@@ -100,6 +100,7 @@ int sizes(int64_t n_arg, int32_t topology, int64_t* nodes, int64_t* actors, int6
 // Layout of one exchange chunk (peer p -> peer q); both ends compute it identically.
 struct Chunk {
     size_t hdir = 0, hslot = 0, hmsg = 0, slot = 0, msg = 0, size = 0;  // byte offsets / total size
+    size_t done = 0;    // full gossip: the sender's done-bitmap words (0: none)
     uint32_t halo = 0;  // halo actors carried (0: none)
     uint32_t hcap = 0;  // halo entries: push-sum messages crossing the face
     uint32_t cap = 0;   // link / receipt entries
@@ -498,13 +499,10 @@ int reset(Handle* h) {
         if (h->generic) {
             HIP_TRY(hipMemsetAsync(h->inc[0] + lo, 0, n * sizeof(uint32_t), h->stream));
             HIP_TRY(hipMemsetAsync(h->inc[1] + lo, 0, n * sizeof(uint32_t), h->stream));
-            if (h->dbits) {  // words lo >> 5 .. (hi - 1) >> 5, then the summary's
-                const size_t w0 = lo >> 5, nw = ((h->hi + 31u) >> 5) - w0;
-                HIP_TRY(hipMemsetAsync(h->dbits + w0, 0, nw * sizeof(uint32_t), h->stream));
-                if (h->dsum) {
-                    const size_t s0 = lo >> 10, ns = ((h->hi + 1023u) >> 10) - s0;
-                    HIP_TRY(hipMemsetAsync(h->dsum + s0, 0, ns * sizeof(uint32_t), h->stream));
-                }
+            if (h->dbits) {  // the whole bitmap (a shard's replica included), then the summary
+                const size_t A = h->g.actors;
+                HIP_TRY(hipMemsetAsync(h->dbits, 0, ((A + 31u) / 32u + 1u) * sizeof(uint32_t), h->stream));
+                if (h->dsum) HIP_TRY(hipMemsetAsync(h->dsum, 0, ((A + 1023u) / 1024u + 1u) * sizeof(uint32_t), h->stream));
             }
             if (h->tally.cnt) {
                 HIP_TRY(hipMemsetAsync(h->tally.chains, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t),
@@ -572,7 +570,7 @@ const char* round_kernel_name(const Handle* h) {
 }
 
 const char* aux_kernel_name(const Handle* h) {
-    if (h->generic) return h->gossip ? "" : "k_scan_* + k_ps_push_fill";
+    if (h->generic) return h->gossip ? (h->sharded && h->world > 1 ? "k_shard_done_out" : "") : "k_scan_* + k_ps_push_fill";
     if (!h->g.has_link || fused_marks(h)) return "";
     if (h->sharded) return h->gossip ? "k_gs_link_scatter_x" : "k_ps_link_scatter_x";
     return "k_link_count";
@@ -650,6 +648,7 @@ int launch_aux(Handle* h, int64_t k, const Xchg* x) {
             if (x) launch_gs_link_scatter_x(a, *x, l);
             else launch_link_count(a, l);
         }
+        if (h->generic && x && h->world > 1) launch_shard_done_out(a, *x, h->stream);
     } else if (h->generic) {
         const int c = (int)(r & 1u);
         launch_exclusive_scan(h->bcnt[c], h->boff[c], h->g.actors, h->scan_scratch, h->stream);
@@ -884,6 +883,10 @@ Chunk chunk_layout(const Handle* h, int p, int q) {
             off = align_up(off + (size_t)kSub * c.hcap * sizeof(double2));
         }
     }
+    if (h->full && h->gossip) {  // the sender's done-bitmap words, words (lo_p >> 5) .. ((hi_p - 1) >> 5)
+        c.done = off;
+        off = align_up(off + (size_t)(((h->abnd[p + 1] - 1) >> 5) - (h->abnd[p] >> 5) + 1) * sizeof(uint32_t));
+    }
     double mean = 0.0, exact = 0.0;
     if (h->full) {
         // every chain of p draws a target uniform over the other actors.  k_gs_full4x picks a
@@ -1008,13 +1011,15 @@ Xchg make_xchg(const Handle* h, void* send, const void* recv) {
             char* b = static_cast<char*>(send) + h->out_off[q];
             const Chunk& c = h->out_chunk[q];
             x.out[q] = PeerOut{reinterpret_cast<ShardHeader*>(b), reinterpret_cast<uint32_t*>(b + c.slot),
-                               c.msg ? reinterpret_cast<double2*>(b + c.msg) : nullptr, c.cap};
+                               c.msg ? reinterpret_cast<double2*>(b + c.msg) : nullptr, c.cap,
+                               c.done ? reinterpret_cast<uint32_t*>(b + c.done) : nullptr};
         }
         if (recv) {
             const char* b = static_cast<const char*>(recv) + h->in_off[q];
             const Chunk& c = h->in_chunk[q];
             x.in[q] = PeerIn{reinterpret_cast<const ShardHeader*>(b), reinterpret_cast<const uint32_t*>(b + c.slot),
-                             c.msg ? reinterpret_cast<const double2*>(b + c.msg) : nullptr, c.cap};
+                             c.msg ? reinterpret_cast<const double2*>(b + c.msg) : nullptr, c.cap,
+                             c.done ? reinterpret_cast<const uint32_t*>(b + c.done) : nullptr};
         }
     }
     // halo faces (side 0: rank-1, side 1: rank+1); the crossing code is -x/+x on a line, -z/+z on a grid
@@ -1404,14 +1409,13 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
         if ((rc = h->alloc(&h->cnt, n, lo)) || (rc = h->alloc(&h->gstate, n, lo))) return bail(rc);
         if (h->generic) {
             if ((rc = h->alloc(&h->inc[0], n, lo)) || (rc = h->alloc(&h->inc[1], n, lo))) return bail(rc);
-            // done bitmap and summary of the own actors (global bit / word numbering)
+            // done bitmap and summary (global bit / word numbering): one GPU, the whole graph; a shard
+            // holds a replica of every rank's bitmap (its own words current, the others' as of the
+            // last exchange), so its senders filter remote targets too
             if (full_quad(h) || h->sharded) {
-                const size_t w0 = lo >> 5, nw = ((h->hi + 31u) >> 5) - w0 + 1;
-                if ((rc = h->alloc(&h->dbits, nw, (int64_t)w0))) return bail(rc);
-                if (n >= kDsumMinActors) {
-                    const size_t s0 = lo >> 10, ns = ((h->hi + 1023u) >> 10) - s0 + 1;
-                    if ((rc = h->alloc(&h->dsum, ns, (int64_t)s0))) return bail(rc);
-                }
+                const size_t nw = ((size_t)A + 31u) / 32u + 1u;
+                if ((rc = h->alloc(&h->dbits, nw))) return bail(rc);
+                if (A >= kDsumMinActors && (rc = h->alloc(&h->dsum, ((size_t)A + 1023u) / 1024u + 1u))) return bail(rc);
             }
             const uint32_t nb = (uint32_t)((n + (1u << kTallyShift) - 1) >> kTallyShift);
             // the tally is a speed path: where its 128 KB of dynamic LDS cannot be allowed (another

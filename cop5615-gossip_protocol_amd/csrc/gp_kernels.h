@@ -142,6 +142,7 @@ struct PeerOut {
     uint32_t* slot;
     double2* msg;
     uint32_t cap;
+    uint32_t* done;  // full gossip: the sender's done-bitmap words (its range), or null
 };
 
 struct PeerIn {
@@ -149,6 +150,7 @@ struct PeerIn {
     const uint32_t* slot;
     const double2* msg;
     uint32_t cap;
+    const uint32_t* done;
 };
 
 // The halo faces of a shard, side 0 = rank-1 (this rank's first plane / the halo below lo),
@@ -231,6 +233,8 @@ struct GsTally {
     uint32_t nb, W;    // buckets; k_gs_full4's grid
 };
 void launch_gs_full4(const RoundArgs& a, const GsTally& t, const Launch& l);  // full gossip, one GPU (lo == 0)
+// full gossip on shards: this rank's done-bitmap words into every peer's chunk (after F(k))
+void launch_shard_done_out(const RoundArgs& a, const Xchg& x, hipStream_t s);
 // the scan, scatter and tally passes of a tallied round (each exits at once otherwise)
 void launch_gs_tally(const RoundArgs& a, const GsTally& t, const Launch& l);
 int prepare_gs_tally();  // once per process: allow the tally pass's 128 KB of dynamic LDS (0: ok)

@@ -1324,6 +1324,21 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
             if (mark) a.act_cur[dir_target(a.g, first + o, x.h.code[side] ^ 1u, 0u) >> kActShift] = mtag;
         }
     }
+    // full gossip: the other ranks' done words into this rank's replica of the bitmap (a word of q's
+    // range that also holds a neighbour's actors, the first and the last, is merged with an atomic OR)
+    if (full && gossip && a.dbits && applied >= 0) {
+        for (uint32_t q = 0; q < x.world; ++q) {
+            if (q == x.rank || !x.in[q].done) continue;
+            const uint32_t w0 = x.abnd[q] >> 5, nw = ((x.abnd[q + 1] - 1u) >> 5) - w0 + 1u;
+            for (uint32_t i = gtid; i < nw; i += gstride) {
+                const uint32_t w = w0 + i, val = x.in[q].done[i];
+                uint32_t now = val;
+                if (i == 0 || i + 1 == nw) now = atomicOr(&a.dbits[w], val) | val;
+                else a.dbits[w] = val;
+                if (a.dsum && now == ~0u) atomicOr(&a.dsum[w >> 5], 1u << (w & 31u));
+            }
+        }
+    }
     // an entry outside this rank's actors / slots can only come from a corrupt chunk: it is
     // reported (GP_EOVERFLOW at the next sync), never written
     const uint32_t elo = full ? a.lo : x.sbnd[x.rank], ehi = full ? a.hi : x.sbnd[x.rank + 1];
@@ -1621,12 +1636,14 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
 
 // Full gossip on a shard of several ranks: k_gs_full4's walk over this rank's actors
 // [lo, hi), four consecutive actors per lane (the quads of the first and last lanes may hold other
-// ranks' actors, which are masked out: neither applied nor emitted).  A receipt for one of this
-// rank's actors takes the sender-side done filter of the one-GPU kernel on this rank's done bitmap
-// (global bit = actor id; its summary from 2^25 actors), then a memory-side atomic; a receipt for
-// another rank's actor becomes an entry of that rank's chunk (the target id), reserved per block and
-// peer.  The receiver drops the entries for its done actors before the atomic (k_shard_unpack): the
-// filter program.fs:92 applies there exactly, on the state after the round the sender ran.
+// ranks' actors, which are masked out: neither applied nor emitted).  Every receipt first takes the
+// sender-side done filter of the one-GPU kernel on this rank's replica of the whole done bitmap
+// (global bit = actor id, its summary from 2^25 actors): its own words are current, the other ranks'
+// arrive with every exchange (k_shard_done_out / k_shard_unpack), a round late at most, which the
+// filter tolerates (done only turns on).  A receipt for one of this rank's actors is then a
+// memory-side atomic; one for another rank's actor an entry of that rank's chunk (the target id),
+// reserved per block and peer.  The receiver drops the entries for its done actors before the
+// atomic (k_shard_unpack): the filter program.fs:92 applies there exactly.
 __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
     const uint32_t r = a.r;
     unsigned long long prev = 0;
@@ -1698,17 +1715,19 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
             }
 #pragma unroll
             for (uint32_t c = 0; c < 2; ++c) {
-                const bool send = tok > c;
                 const bool local = u[c] - lo < hi - lo;
+                // the sender-side done filter on the replica: this rank's own words are current,
+                // another rank's as of the last exchange (stale bits are 0, never 1 too early)
+                uint32_t b = 0;
+                if (tok > c && filter) {
+                    if (a.dsum && ((a.dsum[u[c] >> 10] >> ((u[c] >> 5) & 31u)) & 1u)) b = ~0u;
+                    else b = a.dbits[u[c] >> 5];
+                }
+                const bool send = tok > c && !((b >> (u[c] & 31u)) & 1u);
                 want[2 * j + c] = send && !local;
                 tgt[2 * j + c] = u[c];
                 peer[2 * j + c] = want[2 * j + c] ? owner(x.abnd, x.world, u[c]) : 0u;
-                if (send && local) {
-                    uint32_t b = 0;
-                    if (filter && a.dsum && ((a.dsum[u[c] >> 10] >> ((u[c] >> 5) & 31u)) & 1u)) b = ~0u;
-                    else if (filter) b = a.dbits[u[c] >> 5];
-                    if (!((b >> (u[c] & 31u)) & 1u)) atomicAdd(&a.inc_cur[u[c]], 1u);
-                }
+                if (send && local) atomicAdd(&a.inc_cur[u[c]], 1u);
             }
         }
         // sub-segment by the block-iteration's 1024-actor chunk (its first quad / 256, block-uniform):
@@ -1735,6 +1754,17 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
         }
     }
     if (r) block_add(newly, a.parts, (long long)r - 1);
+}
+
+// Full gossip on shards: this rank's words of the done bitmap (after F(r)) into every peer's chunk.
+__global__ __launch_bounds__(kBlock) void k_shard_done_out(RoundArgs a, Xchg x) {
+    if (applied_converged(a)) return;  // block-uniform
+    const uint32_t w0 = a.lo >> 5, nw = ((a.hi - 1u) >> 5) - w0 + 1u;
+    for (uint32_t q = 0; q < x.world; ++q) {
+        if (q == x.rank || !x.out[q].done) continue;
+        uint32_t* o = x.out[q].done;
+        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nw; i += gridDim.x * kBlock) o[i] = a.dbits[w0 + i];
+    }
 }
 
 // Tallied round: place every receipt of F(r) into its bucket's segment, at this workgroup's
@@ -2297,6 +2327,13 @@ void launch_ps_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l
 
 void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l) {
     if (const unsigned b = scatter_blocks(a)) hipLaunchKernelGGL(k_gs_link_scatter_x, dim3(b), dim3(kBlock), 0, l.stream, a, x);
+}
+
+void launch_shard_done_out(const RoundArgs& a, const Xchg& x, hipStream_t s) {
+    const uint32_t nw = ((a.hi - 1u) >> 5) - (a.lo >> 5) + 1u;
+    uint32_t blocks = (nw + kBlock - 1) / kBlock;
+    blocks = blocks > 1024u ? 1024u : blocks;
+    hipLaunchKernelGGL(k_shard_done_out, dim3(blocks), dim3(kBlock), 0, s, a, x);
 }
 
 void launch_gs_full4x(const RoundArgs& a, const Xchg& x, const Launch& l) {
