@@ -1331,10 +1331,12 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
             if (q == x.rank || !x.in[q].done) continue;
             const uint32_t w0 = x.abnd[q] >> 5, nw = ((x.abnd[q + 1] - 1u) >> 5) - w0 + 1u;
             for (uint32_t i = gtid; i < nw; i += gstride) {
-                const uint32_t w = w0 + i, val = x.in[q].done[i];
+                const uint32_t w = w0 + i, val = x.in[q].done[i], old = a.dbits[w];
+                if ((old | val) == old) continue;  // nothing new (most words, most rounds)
                 uint32_t now = val;
                 if (i == 0 || i + 1 == nw) now = atomicOr(&a.dbits[w], val) | val;
                 else a.dbits[w] = val;
+                // the summary bit of a word that just filled (one atomic per such word, not per round)
                 if (a.dsum && now == ~0u) atomicOr(&a.dsum[w >> 5], 1u << (w & 31u));
             }
         }
