@@ -126,6 +126,13 @@ struct Ckpt {
     uint8_t* flags = nullptr;
     uint8_t* act = nullptr;
     unsigned long long* work = nullptr;
+    // full gossip: the counts, states, round k0-1's receipts and the done-bitmap replica
+    uint32_t* cnt = nullptr;
+    uint8_t* gstate = nullptr;
+    uint32_t* inc = nullptr;
+    uint32_t* dbits = nullptr;
+    uint32_t* dsum = nullptr;
+    bool allocated = false;
 };
 
 struct Handle {
@@ -461,6 +468,10 @@ int clear_act(Handle* h, int i) {
     return GP_OK;
 }
 
+// Full gossip's done bitmap over every actor (one bit each) and its summary (one bit per word).
+size_t dbits_words_all(const Handle* h) { return ((size_t)h->g.actors + 31u) / 32u + 1u; }
+size_t dsum_words_all(const Handle* h) { return ((size_t)h->g.actors + 1023u) / 1024u + 1u; }
+
 void full_plan(Handle* h);
 
 int reset(Handle* h) {
@@ -500,9 +511,8 @@ int reset(Handle* h) {
             HIP_TRY(hipMemsetAsync(h->inc[0] + lo, 0, n * sizeof(uint32_t), h->stream));
             HIP_TRY(hipMemsetAsync(h->inc[1] + lo, 0, n * sizeof(uint32_t), h->stream));
             if (h->dbits) {  // the whole bitmap (a shard's replica included), then the summary
-                const size_t A = h->g.actors;
-                HIP_TRY(hipMemsetAsync(h->dbits, 0, ((A + 31u) / 32u + 1u) * sizeof(uint32_t), h->stream));
-                if (h->dsum) HIP_TRY(hipMemsetAsync(h->dsum, 0, ((A + 1023u) / 1024u + 1u) * sizeof(uint32_t), h->stream));
+                HIP_TRY(hipMemsetAsync(h->dbits, 0, dbits_words_all(h) * sizeof(uint32_t), h->stream));
+                if (h->dsum) HIP_TRY(hipMemsetAsync(h->dsum, 0, dsum_words_all(h) * sizeof(uint32_t), h->stream));
             }
             if (h->tally.cnt) {
                 HIP_TRY(hipMemsetAsync(h->tally.chains, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t),
@@ -1123,8 +1133,12 @@ int shard_deliver(Handle* h, const void* recv) {
 constexpr int64_t kCkptEvery = 256;
 
 bool tiers_on(const Handle* h) {
-    return h->sharded && h->world > 1 && !h->gossip && !h->generic && !(h->cfg.flags & GP_FLAG_FULL_PLAN);
+    // push-sum on the pull path, and full gossip (its remote receipts thin out as targets report:
+    // the senders filter them on the replicated done bitmap)
+    const bool ps = !h->gossip && !h->generic, fg = h->gossip && h->full;
+    return h->sharded && h->world > 1 && (ps || fg) && !(h->cfg.flags & GP_FLAG_FULL_PLAN);
 }
+
 
 uint32_t tier_cap(uint32_t full, uint32_t m, bool tight) {
     const uint64_t need = tight ? (uint64_t)m : 2ull * m + 64u;
@@ -1135,14 +1149,23 @@ uint32_t tier_cap(uint32_t full, uint32_t m, bool tight) {
 
 int ensure_ckpt(Handle* h) {
     Ckpt& c = h->ck;
-    if (c.msg) return GP_OK;
+    if (c.allocated) return GP_OK;
     const size_t xn = (size_t)(h->ext_hi() - h->ext_lo()), n = h->own();
-    const size_t nsl = (size_t)(h->sbnd.empty() ? 0 : h->sbnd[h->rank + 1] - h->sbnd[h->rank]);
     int rc;
+    if (h->gossip) {  // full gossip
+        if ((rc = h->alloc(&c.cnt, n)) || (rc = h->alloc(&c.gstate, n)) || (rc = h->alloc(&c.inc, n)) ||
+            (rc = h->alloc(&c.dbits, dbits_words_all(h))))
+            return rc;
+        if (h->dsum && (rc = h->alloc(&c.dsum, dsum_words_all(h)))) return rc;
+        c.allocated = true;
+        return GP_OK;
+    }
+    const size_t nsl = (size_t)(h->sbnd.empty() ? 0 : h->sbnd[h->rank + 1] - h->sbnd[h->rank]);
     if ((rc = h->alloc(&c.msg, xn)) || (rc = h->alloc(&c.dir, xn)) || (rc = h->alloc(&c.flags, n))) return rc;
     if (h->work && (rc = h->alloc(&c.work, (size_t)kParts * kWorkStride))) return rc;
     if (h->lcnt[0] && ((rc = h->alloc(&c.lcnt, nsl)) || (rc = h->alloc(&c.rmsg, nsl)))) return rc;
     if (h->act[0] && (rc = h->alloc(&c.act, act_bytes(h)))) return rc;
+    c.allocated = true;
     return GP_OK;
 }
 
@@ -1157,6 +1180,15 @@ int ckpt_copy(Handle* h, bool save) {
         return save ? hipMemcpyAsync(saved, live, bytes, hipMemcpyDeviceToDevice, s)
                     : hipMemcpyAsync(live, saved, bytes, hipMemcpyDeviceToDevice, s);
     };
+    if (h->gossip) {  // full gossip: F(k0) reads cnt, gstate, the receipts of round k0-1 and the replica
+        HIP_TRY(cp(h->cnt + lo, c.cnt, n * sizeof(uint32_t)));
+        HIP_TRY(cp(h->gstate + lo, c.gstate, n));
+        HIP_TRY(cp(h->inc[p] + lo, c.inc, n * sizeof(uint32_t)));
+        HIP_TRY(cp(h->dbits, c.dbits, dbits_words_all(h) * sizeof(uint32_t)));
+        if (h->dsum) HIP_TRY(cp(h->dsum, c.dsum, dsum_words_all(h) * sizeof(uint32_t)));
+        // round k0's receipts accumulate in the other array, empty before F(k0): a failed batch's go
+        if (!save) HIP_TRY(hipMemsetAsync(h->inc[p ^ 1] + lo, 0, n * sizeof(uint32_t), s));
+    } else {
     HIP_TRY(cp(h->msg[p] + xlo, c.msg, xn * sizeof(double2)));
     HIP_TRY(cp(h->dir[p] + xlo, c.dir, xn));
     HIP_TRY(cp(h->flags + lo, c.flags, n));
@@ -1169,6 +1201,7 @@ int ckpt_copy(Handle* h, bool save) {
         if (!save) HIP_TRY(hipMemsetAsync(h->lcnt[p ^ 1] + slo, 0, nsl, s));
     }
     if (h->act[0]) HIP_TRY(cp(h->act[k0 & 1] + act_first(h), c.act, act_bytes(h)));
+    }
     if (save) {
         c.next_kernel = k0;
         c.rounds = h->rounds;
@@ -1413,9 +1446,8 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
             // holds a replica of every rank's bitmap (its own words current, the others' as of the
             // last exchange), so its senders filter remote targets too
             if (full_quad(h) || h->sharded) {
-                const size_t nw = ((size_t)A + 31u) / 32u + 1u;
-                if ((rc = h->alloc(&h->dbits, nw))) return bail(rc);
-                if (A >= kDsumMinActors && (rc = h->alloc(&h->dsum, ((size_t)A + 1023u) / 1024u + 1u))) return bail(rc);
+                if ((rc = h->alloc(&h->dbits, dbits_words_all(h)))) return bail(rc);
+                if (A >= kDsumMinActors && (rc = h->alloc(&h->dsum, dsum_words_all(h)))) return bail(rc);
             }
             const uint32_t nb = (uint32_t)((n + (1u << kTallyShift) - 1) >> kTallyShift);
             // the tally is a speed path: where its 128 KB of dynamic LDS cannot be allowed (another

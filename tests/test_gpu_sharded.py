@@ -252,6 +252,29 @@ def test_shards_activity_tiers_default():
         e.close()
 
 
+@pytest.mark.parametrize("n,world,seed", [(1000, 2, 1), (20000, 3, 4), (100000, 5, 2), (300000, 8, 6)])
+def test_full_gossip_tight_tiers_vs_oracle(n, world, seed):
+    """Full gossip on shards with tight activity tiers: the senders filter remote receipts on the
+    replicated done bitmap, the chunks shrink with the receipts still sent, overflowed batches are
+    replayed from restore points (cnt, states, receipts, the replica) — bit-exact against the oracle,
+    twice (after a reset)."""
+    ref = oracle.OracleSim(n, "full", "gossip", seed=seed)
+    rs = ref.step(threads=8)
+    engines = _shards(n, "full", "gossip", world, seed, tight_tiers=True)
+    for _ in range(2):
+        sts = sharded.run_local(engines)
+        for st in sts:
+            assert (st.round, st.completed, st.converged) == (rs.round, rs.completed, rs.converged)
+        _check_vs(ref, engines, "gossip")
+        for e in engines:
+            e.reset()
+    if n >= 100000:
+        ss = [e.shard_stats() for e in engines]
+        assert all(x["plan_changes"] > 0 for x in ss), ss
+    for e in engines:
+        e.close()
+
+
 @pytest.mark.parametrize("n,topo,world,seed", [(20000, "Imp3D", 3, 5), (300000, "Imp3D", 8, 11)])
 def test_group_tight_tiers_vs_oracle(n, topo, world, seed):
     """The library's multi-GPU engine (gp_step over num_gpus shards, here on one device) with
