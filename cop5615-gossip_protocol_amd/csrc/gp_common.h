@@ -33,12 +33,12 @@ __host__ __device__ __forceinline__ uint4 philox(uint32_t v, uint32_t r, uint32_
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-        const uint32_t hi0 = mulhi32(kPhiloxM0, c0), lo0 = kPhiloxM0 * c0;
-        const uint32_t hi1 = mulhi32(kPhiloxM1, c2), lo1 = kPhiloxM1 * c2;
-        c0 = hi1 ^ c1 ^ k0;
-        c1 = lo1;
-        c2 = hi0 ^ c3 ^ k1;
-        c3 = lo0;
+        // 32x32->64 products: one v_mad_u64_u32 each on gfx950 (a mul_hi + mul_lo pair otherwise)
+        const uint64_t p0 = (uint64_t)kPhiloxM0 * c0, p1 = (uint64_t)kPhiloxM1 * c2;
+        c0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        c1 = (uint32_t)p1;
+        c2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c3 = (uint32_t)p0;
         k0 += kPhiloxW0;
         k1 += kPhiloxW1;
     }

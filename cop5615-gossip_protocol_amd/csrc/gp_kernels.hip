@@ -1283,6 +1283,36 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(RoundArgs a, Xchg x, long
 
 // total[applied] = total[applied-1] + every rank's count; the received link entries land in
 // their CSR slots (push-sum (s,w) / gossip chain count) or, for "full" gossip, as receipts.
+// The used entries of a chunk's kSub sub-segments (`cap` entries each, the first count[sb] used)
+// as one index range [0, total): the counts are read once, together, and an index is mapped to its
+// entry with 15 compares (a walk over every sub-segment's capacity visits mostly unused entries in
+// a quiet round; one loop per sub-segment waits on each count in turn).
+struct SubWalk {
+    uint32_t pre[kSub], cap, total;
+    __device__ __forceinline__ SubWalk(const uint32_t* count, uint32_t c) : cap(c) {
+        uint32_t n[kSub];
+#pragma unroll
+        for (uint32_t sb = 0; sb < kSub; ++sb) n[sb] = count[sb];
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t sb = 0; sb < kSub; ++sb) {
+            pre[sb] = t;
+            t += n[sb] < c ? n[sb] : c;  // a count past the capacity overflowed: those entries were not written
+        }
+        total = t;
+    }
+    __device__ __forceinline__ uint32_t at(uint32_t v) const {
+        uint32_t sb = 0, base = 0;
+#pragma unroll
+        for (uint32_t k = 1; k < kSub; ++k)
+            if (v >= pre[k]) {
+                sb = k;
+                base = pre[k];
+            }
+        return sb * cap + (v - base);
+    }
+};
+
 __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, long long applied, int gossip,
                                                           int full) {
     if (blockIdx.x == 0 && threadIdx.x == 0 && applied >= 0) {
@@ -1311,9 +1341,9 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
         for (uint32_t i = gtid; i < n; i += gstride) a.dir_cur[first + i] = idir[i];
         if (!x.h.in_slot[side]) continue;
         const uint32_t cap = x.h.in_cap[side];
-        for (uint32_t i = gtid; i < kSub * cap; i += gstride) {  // one pass over every sub-segment
-            const uint32_t sb = i / cap;
-            if (i - sb * cap >= x.h.in_hdr[side]->nhalo[sb]) continue;
+        const SubWalk w(x.h.in_hdr[side]->nhalo, cap);
+        for (uint32_t v = gtid; v < w.total; v += gstride) {
+            const uint32_t i = w.at(v);
             const uint32_t o = x.h.in_slot[side][i];
             if (o >= n) {
                 atomicOr(x.overflow, 2u);
@@ -1350,10 +1380,11 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
     const uint32_t q = blockIdx.x / bpp;
     if (q < x.world && q != x.rank && x.in[q].cap) {
         const PeerIn& in = x.in[q];
-        // kSub sub-segments of `cap` entries; entries past a sub-segment's count are unused
-        for (uint32_t i = (blockIdx.x % bpp) * kBlock + threadIdx.x; i < kSub * in.cap; i += bpp * kBlock) {
-            const uint32_t sb = i / in.cap;
-            if (i - sb * in.cap >= in.hdr->nlinks[sb]) continue;
+        // kSub sub-segments of `cap` entries, each walked up to its count only (a chunk sized for an
+        // all-sending round holds a few entries in most rounds)
+        const SubWalk w(in.hdr->nlinks, in.cap);
+        for (uint32_t v = (blockIdx.x % bpp) * kBlock + threadIdx.x; v < w.total; v += bpp * kBlock) {
+            const uint32_t i = w.at(v);
             const uint32_t e = in.slot[i];
             const uint32_t t = (gossip && !full) ? e & 0x7FFFFFFFu : e;
             if (t < elo || t >= ehi) {
@@ -1736,10 +1767,15 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
         // consecutive chunks of the range cycle through the kSub sub-segments whatever the grid, so
         // gp_api.cpp sizes a sub-segment for ceil(chunks / kSub) chunks
         const uint32_t sub = ((q - threadIdx.x) >> 8) % kSub;
-        block_reserve(x, want, peer, pos, sub);
+        bool any = false;
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k)
-            if (want[k]) put<false>(x, peer[k], pos[k], tgt[k], make_double2(0.0, 0.0), sub);
+        for (uint32_t k = 0; k < 8; ++k) any |= want[k];
+        if (__syncthreads_or(any)) {  // block-uniform: most block-iterations of a quiet round send nothing
+            block_reserve(x, want, peer, pos, sub);
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k)
+                if (want[k]) put<false>(x, peer[k], pos[k], tgt[k], make_double2(0.0, 0.0), sub);
+        }
         // the reports of this round into the done bitmap: 8 lanes = 32 actors = one word
         uint32_t w = done4 << ((q & 7u) * 4u);
         w |= __shfl_xor(w, 1, 64);

@@ -34,14 +34,17 @@ def main():
         per[rnd][n] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     nodes = d.get("nodes") or max(trace)
     prev = [0] + trace[:-1]
-    phases = {"dense (<1% converged)": lambda c: c * 100 < nodes, "tail (>=99% converged)": lambda c: c * 100 >= 99 * nodes}
+    phases = {"dense (<1% converged)": lambda c: c * 100 < nodes,
+              "mid (1-99% converged)": lambda c: nodes <= c * 100 < 99 * nodes,
+              "tail (>=99% converged)": lambda c: c * 100 >= 99 * nodes,
+              "whole run": lambda c: True}
     for label, test in phases.items():
         rs = [r for r in per if r < len(prev) and test(prev[r])]
         if not rs:
             continue
         ks = sorted({k for r in rs for k in per[r]}, key=lambda k: -sum(per[r].get(k, 0.0) for r in rs))
         tot = statistics.fmean(sum(per[r].values()) for r in rs) / world
-        print(f"{label}: {len(rs)} rounds, kernels per rank-round {tot:.1f} us")
+        print(f"{label}: {len(rs)} rounds, kernels per rank-round {tot:.1f} us, per rank over these rounds {tot * len(rs) / 1e3:.2f} ms")
         for k in ks:
             print(f"  {k:48s} {statistics.fmean(per[r].get(k, 0.0) for r in rs) / world:9.2f} us")
 
