@@ -664,8 +664,12 @@ int launch_aux(Handle* h, int64_t k, const Xchg* x) {
         launch_exclusive_scan(h->bcnt[c], h->boff[c], h->g.actors, h->scan_scratch, h->stream);
         launch_ps_push_fill(a, h->slot[c], h->boff[c], l);
     } else if (h->g.has_link) {
-        if (x) launch_ps_link_scatter_x(a, *x, l);
-        else if (!fused_marks(h)) launch_link_count(a, l);
+        // a shard's quiet-tail rounds route their own link messages (k_ps_quiet_x) and the pass would
+        // return at once: once the synced count has reached act_thr, every later round is such a round
+        // (the count only grows), so the pass is not launched at all
+        const bool tail = h->act[0] && h->act_thr && h->completed >= (int64_t)h->act_thr && k >= h->rounds + 1;
+        if (x && !tail) launch_ps_link_scatter_x(a, *x, l);
+        else if (!x && !fused_marks(h)) launch_link_count(a, l);
     }
     return GP_OK;
 }

@@ -1341,6 +1341,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
         for (uint32_t i = gtid; i < n; i += gstride) a.dir_cur[first + i] = idir[i];
         if (!x.h.in_slot[side]) continue;
         const uint32_t cap = x.h.in_cap[side];
+        if (gtid >= kSub * cap) continue;  // no entry for this thread (a tail round's chunks are small)
         const SubWalk w(x.h.in_hdr[side]->nhalo, cap);
         for (uint32_t v = gtid; v < w.total; v += gstride) {
             const uint32_t i = w.at(v);
@@ -1378,7 +1379,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
     // flight together (one peer after another left each thread a chain of dependent loads per peer)
     const uint32_t bpp = gridDim.x / x.world;
     const uint32_t q = blockIdx.x / bpp;
-    if (q < x.world && q != x.rank && x.in[q].cap) {
+    if (q < x.world && q != x.rank && x.in[q].cap && (blockIdx.x % bpp) * kBlock + threadIdx.x < kSub * x.in[q].cap) {
         const PeerIn& in = x.in[q];
         // kSub sub-segments of `cap` entries, each walked up to its count only (a chunk sized for an
         // all-sending round holds a few entries in most rounds)
