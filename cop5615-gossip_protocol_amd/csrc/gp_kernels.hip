@@ -1533,7 +1533,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_push(RoundArgs a) { gs_push_body<
 // receipt is one the receiver would have dropped, and a stale 0 bit only costs an atomic.  The
 // filter is applied only once 1/GP_GS_FILTER_DIV of the actors have reported (a bit read costs
 // less than the atomic it saves only when enough targets are done).  A summary bitmap `dsum`
-// (one bit per 32-actor word of dbits, set when the word fills: 98 KB at 100M actors, L2-resident)
+// (one bit per 32-actor word of dbits, set when the word fills: 391 KB at 100M actors, L2-resident)
 // answers for targets in all-done words, so the long tail of a run, where nearly every target is
 // done, reads the 12.5 MB bitmap rarely (from 2^25 actors: C4 -7.5%; where dbits fits an L2 the
 // extra dependent load cost more, 10M +36%, profiles/round3/c4_tally/cli_dsum.txt).
