@@ -1111,8 +1111,13 @@ int shard_deliver(Handle* h, const void* recv) {
     // the halo faces (rank-1's last actors land below lo, rank+1's first at hi) and the link
     // entries are applied by one kernel
     const Xchg x = make_xchg(h, h->pending_send, recv);
-    launch_shard_unpack(h->args((uint32_t)k), x, applied_round(h, k), std::max(kSub * h->max_in_cap, h->halo),
-                        h->gossip ? 1 : 0, h->full ? 1 : 0, h->stream);
+    // the grid covers the largest per-peer part: link entries, a halo face, or (full gossip) a
+    // peer's done-bitmap words, which arrive whole whatever the plan
+    uint32_t most = std::max(kSub * h->max_in_cap, h->halo);
+    if (h->gossip && h->full)
+        for (int q = 0; q < h->world; ++q) most = std::max(most, (uint32_t)((h->abnd[q + 1] - h->abnd[q]) / 32 + 2));
+    launch_shard_unpack(h->args((uint32_t)k), x, applied_round(h, k), most, h->gossip ? 1 : 0, h->full ? 1 : 0,
+                        h->stream);
     HIP_TRY(hipGetLastError());
     h->awaiting_deliver = false;
     h->last_recv = recv;
@@ -1691,8 +1696,12 @@ int group_step(Handle* h, int64_t max_rounds, gp_status* st) {
                 if ((rc = shard_deliver(G.shard[p], G.recv[p]))) return rc;
             }
         }
+        const int64_t before = G.completed;
         if ((rc = group_sync(G, sts))) return rc;
-        G.batch = std::min<int64_t>(G.batch * 2, 64);
+        // batches start again from 8 rounds when the run enters the half-reported phase, where the
+        // activity tiers begin (a plan is chosen at every sync; sharded.py _next_batch does the same)
+        const int64_t nodes = G.shard[0]->lay.nodes;
+        G.batch = (2 * before < nodes && nodes <= 2 * G.completed) ? 8 : std::min<int64_t>(G.batch * 2, 64);
     }
     if (sts.empty() && (rc = group_sync(G, sts))) return rc;
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -272,11 +272,25 @@ def run(engine, transport, max_rounds: int = 1 << 40, batch: int = 8, max_batch:
             engine.deliver()
             if ev:
                 ev[3].record()
+        before = int(st.completed)  # (sync() may refill the same status object)
         st = engine.sync()
         if timer:
             timer.collect()
-        batch = min(batch * 2, max_batch)
+        batch = _next_batch(batch, max_batch, _nodes(engine), before, int(st.completed))
     return st
+
+
+def _nodes(engine) -> int:
+    return int(engine.layout.nodes)  # HipShard and the oracle's shard engine alike
+
+
+def _next_batch(batch: int, max_batch: int, nodes: int, before: int, after: int) -> int:
+    """Batches double up to max_batch; they start again from 8 rounds when the run enters the
+    half-reported phase, where the activity tiers begin (the plan is chosen at every sync, and a
+    short run such as full gossip would otherwise reach its end inside one long batch)."""
+    if 2 * before < nodes <= 2 * after:
+        return 8
+    return min(batch * 2, max_batch)
 
 
 def run_local(engines, max_rounds: int = 1 << 40, batch: int = 8, max_batch: int = 64):
@@ -292,7 +306,8 @@ def run_local(engines, max_rounds: int = 1 << 40, batch: int = 8, max_batch: int
             t.exchange_all(engines)
             for e in engines:
                 e.deliver()
+        before = int(sts[0].completed)
         sts = [e.sync() for e in engines]
         assert len({(int(s.round), int(s.completed), int(s.converged)) for s in sts}) == 1, "shards disagree"
-        batch = min(batch * 2, max_batch)
+        batch = _next_batch(batch, max_batch, _nodes(engines[0]), before, int(sts[0].completed))
     return sts

@@ -193,3 +193,14 @@ def test_dist_shard_job_script_gloo(world, case):
     for k in want:
         np.testing.assert_array_equal(got[k], want[k])
     ref.close()
+
+
+def test_batch_schedule_restarts_at_half_reported():
+    """The host loop's batches double up to the cap and start again from 8 rounds at the sync
+    where the run passes half of the nodes reported (the activity tiers' first decision)."""
+    from gossip_amd.sharded import _next_batch
+    assert _next_batch(8, 64, 1000, 0, 10) == 16
+    assert _next_batch(64, 64, 1000, 0, 10) == 64
+    assert _next_batch(32, 64, 1000, 499, 500) == 8
+    assert _next_batch(32, 64, 1000, 100, 999) == 8
+    assert _next_batch(8, 64, 1000, 500, 600) == 16  # already past half: no restart

@@ -69,10 +69,11 @@ while not sts[0].converged and sts[0].round < cap:
                 ev[4].record()
         ev[5].record()
         events.append(ev)
+    before = int(sts[0].completed)
     sts = [e.sync() for e in shards]
     assert len({(int(s.round), int(s.completed), int(s.converged)) for s in sts}) == 1, "shards disagree"
     send_bytes.append((int(sts[0].round), sum(shards[0].send_splits)))  # rank 0's plan from here on
-    batch = min(batch * 2, 64)
+    batch = sharded._next_batch(batch, 64, nodes, before, int(sts[0].completed))  # the product loop's schedule
 torch.cuda.synchronize()
 el = time.perf_counter() - t0
 rounds = int(sts[0].round)
