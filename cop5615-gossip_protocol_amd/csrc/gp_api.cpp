@@ -632,7 +632,15 @@ void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed) {
             if (x) launch_gs_full4x(a, *x, l);
             else if (full_quad(h)) {
                 launch_gs_full4(a, h->tally, l);
-                launch_gs_tally(a, h->tally, l);
+                // the tally's passes exit at once in a round that does not tally; once the synced count
+                // rules the tally out for every later round (fewer than 1/kTallyLateDiv of the nodes
+                // left, and fewer receipts to them than thr even at two chains per actor), they are
+                // not launched at all
+                const int64_t left = h->lay.nodes - h->completed;
+                // (F(k) decides on the count after round k - 2: at least the synced one from k = rounds + 2)
+                const bool never = h->tally.thr && k >= h->rounds + 2 && left * (int64_t)std::max<uint64_t>(kTallyLateDiv, 1) < h->lay.nodes &&
+                                   (double)left * 2.0 * (double)h->g.actors < (double)h->tally.thr * (double)h->lay.nodes;
+                if (!never) launch_gs_tally(a, h->tally, l);
             }
             else launch_gs_push(a, l);
         } else {

@@ -221,6 +221,10 @@ void launch_gs_push(const RoundArgs& a, const Launch& l);
 // inc_cur whole.  Receipts to done targets are not filtered there (the receiver drops them).
 constexpr uint32_t kTallyShift = 15;          // 32768 targets per bucket: 128 KB of LDS counters
 constexpr uint32_t kMaxTallyBuckets = 4096;   // k_gs_full4's LDS counters: 16 KB at most
+#ifndef GP_TALLY_LATE_DIV
+#define GP_TALLY_LATE_DIV 64  // A/B knob; 0: no late tally
+#endif
+constexpr uint64_t kTallyLateDiv = GP_TALLY_LATE_DIV;  // also tally (filter on) while >= 1/64 of the nodes are not done
 struct GsTally {
     uint32_t* cnt;     // [nb * W] receipts per (bucket, workgroup), bucket-major; null: no tally
     uint32_t* off;     // [nb * W + 1] exclusive scan of cnt

@@ -1555,8 +1555,16 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
     // the same final counts); block 0 records the choice for the passes after this kernel
     // (the chains of round r - 1 that reach a target not done yet: the atomics round r would issue,
     // estimated from the share of nodes not done)
+    // Late rounds too, while at least 1/kTallyLateDiv of the nodes are not done, on graphs whose done
+    // bitmap outgrows an L2 (those with the summary): there the sender filter's bitmap reads (most
+    // summary words not yet full) cost more per draw than the tally's passes (C4: 2.2 vs 1.67 ms per
+    // round at 90-97% reported, C4 60.1 -> 58.3 ms; at 10M the bitmap is L2-resident and the filter
+    // wins, +3.5% with the rule: profiles/round4/c4_late_tally/)
+    const double ch = (t.cnt && r >= 1u) ? (double)tally_chains(t, r - 1u) : 0.0;  // (no tally: no chains array)
     const bool tally = t.cnt && r >= 1u && prev < a.target &&
-                       (double)tally_chains(t, r - 1u) * (double)(a.target - prev) >= (double)t.thr * (double)a.target;
+                       (ch * (double)(a.target - prev) >= (double)t.thr * (double)a.target ||
+                        (kTallyLateDiv && a.dsum && (unsigned long long)GP_GS_FILTER_DIV * prev >= a.target &&
+                         (unsigned long long)(a.target - prev) * kTallyLateDiv >= a.target && ch >= (double)t.thr));
     if (t.cnt && blockIdx.x == 0 && threadIdx.x < 64) {
         *part_slot(t.chains, r + 2u, threadIdx.x) = 0u;  // the slot round r + 2 adds into
         if (threadIdx.x == 0) t.on[r & 3u] = tally ? 1u : 0u;
