@@ -637,8 +637,9 @@ void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed) {
                 // left, and fewer receipts to them than thr even at two chains per actor), they are
                 // not launched at all
                 const int64_t left = h->lay.nodes - h->completed;
-                // (F(k) decides on the count after round k - 2: at least the synced one from k = rounds + 2)
-                const bool never = h->tally.thr && k >= h->rounds + 2 && left * (int64_t)std::max<uint64_t>(kTallyLateDiv, 1) < h->lay.nodes &&
+                // (round k's choice is made by F(k - 1) on the count after round k - 3: at least the
+                // synced one from k = rounds + 2; one round of margin)
+                const bool never = h->tally.thr && k >= h->rounds + 3 && left * (int64_t)std::max<uint64_t>(kTallyLateDiv, 1) < h->lay.nodes &&
                                    (double)left * 2.0 * (double)h->g.actors < (double)h->tally.thr * (double)h->lay.nodes;
                 if (!never) launch_gs_tally(a, h->tally, l);
             }

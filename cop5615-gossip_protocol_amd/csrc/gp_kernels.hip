@@ -1551,23 +1551,25 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
     const uint32_t r = a.r;
     unsigned long long prev = 0;
     if (r) prev = gate_count(a, (long long)r - 1);
-    // tally this round: the previous one emitted at least thr chains (uniform: every block reads
-    // the same final counts); block 0 records the choice for the passes after this kernel
-    // (the chains of round r - 1 that reach a target not done yet: the atomics round r would issue,
-    // estimated from the share of nodes not done)
-    // Late rounds too, while at least 1/kTallyLateDiv of the nodes are not done, on graphs whose done
-    // bitmap outgrows an L2 (those with the summary): there the sender filter's bitmap reads (most
-    // summary words not yet full) cost more per draw than the tally's passes (C4: 2.2 vs 1.67 ms per
-    // round at 90-97% reported, C4 60.1 -> 58.3 ms; at 10M the bitmap is L2-resident and the filter
-    // wins, +3.5% with the rule: profiles/round4/c4_late_tally/)
+    // Round r tallies as F(r - 1) decided (t.on[r & 3]).  F(r) decides for round r + 1, one round
+    // ahead, so that it can leave the receipt words of round r + 1 unzeroed when that round tallies
+    // (its count pass writes them whole): 400 MB of stores less per tallied round at C4.  The rule:
+    // the chains of round r - 1 that reach a target not done yet (the atomics a round would issue,
+    // estimated from the share of nodes not done after round r - 2) reach thr; or, late in the run,
+    // while at least 1/kTallyLateDiv of the nodes are not done, on graphs whose done bitmap outgrows
+    // an L2 (those with the summary): there the sender filter's bitmap reads (most summary words not
+    // yet full) cost more per draw than the tally's passes (C4: 2.2 vs 1.67 ms per round at 90-97%
+    // reported; at 10M the bitmap is L2-resident and the filter wins: profiles/round4/c4_late_tally/).
+    // Uniform: every block reads the same final counts.
+    const bool tally = t.cnt && r >= 1u && t.on[r & 3u];
     const double ch = (t.cnt && r >= 1u) ? (double)tally_chains(t, r - 1u) : 0.0;  // (no tally: no chains array)
-    const bool tally = t.cnt && r >= 1u && prev < a.target &&
-                       (ch * (double)(a.target - prev) >= (double)t.thr * (double)a.target ||
-                        (kTallyLateDiv && a.dsum && (unsigned long long)GP_GS_FILTER_DIV * prev >= a.target &&
-                         (unsigned long long)(a.target - prev) * kTallyLateDiv >= a.target && ch >= (double)t.thr));
+    const bool tally_next = t.cnt && r >= 1u && prev < a.target &&
+                            (ch * (double)(a.target - prev) >= (double)t.thr * (double)a.target ||
+                             (kTallyLateDiv && a.dsum && (unsigned long long)GP_GS_FILTER_DIV * prev >= a.target &&
+                              (unsigned long long)(a.target - prev) * kTallyLateDiv >= a.target && ch >= (double)t.thr));
     if (t.cnt && blockIdx.x == 0 && threadIdx.x < 64) {
         *part_slot(t.chains, r + 2u, threadIdx.x) = 0u;  // the slot round r + 2 adds into
-        if (threadIdx.x == 0) t.on[r & 3u] = tally ? 1u : 0u;
+        if (threadIdx.x == 0) t.on[(r + 1u) & 3u] = tally_next ? 1u : 0u;
     }
     if (r && prev >= a.target) return;
     if (tally) {
@@ -1595,7 +1597,8 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
             for (uint32_t j = 0; j < 4; ++j)
                 if (v0 + j >= na) inc[j] = 0u;  // the padding past the last actor
             if (inc[0] | inc[1] | inc[2] | inc[3]) {
-                *reinterpret_cast<uint4*>(a.inc_prev + v0) = make_uint4(0u, 0u, 0u, 0u);
+                // consumed; round r + 1 adds its receipts here (a tallied round writes them whole)
+                if (!tally_next) *reinterpret_cast<uint4*>(a.inc_prev + v0) = make_uint4(0u, 0u, 0u, 0u);
                 uint4 c4 = *reinterpret_cast<const uint4*>(a.cnt + v0);
                 uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
                 const uint32_t st0 = st4;
