@@ -1571,7 +1571,12 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
         *part_slot(t.chains, r + 2u, threadIdx.x) = 0u;  // the slot round r + 2 adds into
         if (threadIdx.x == 0) t.on[(r + 1u) & 3u] = tally_next ? 1u : 0u;
     }
-    if (r && prev >= a.target) return;
+    if (r && prev >= a.target) {
+        // past convergence (the choice was made on an older count): this round's passes must not run
+        // on counts this kernel did not write
+        if (t.cnt && blockIdx.x == 0 && threadIdx.x == 0) t.on[r & 3u] = 0u;
+        return;
+    }
     if (tally) {
         for (uint32_t i = threadIdx.x; i < t.nb; i += kBlock) tcnt[i] = 0u;
         __syncthreads();
