@@ -1359,7 +1359,9 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
     // range that also holds a neighbour's actors, the first and the last, is merged with an atomic OR)
     if (full && gossip && a.dbits && applied >= 0) {
         for (uint32_t q = 0; q < x.world; ++q) {
-            if (q == x.rank || !x.in[q].done) continue;
+            // a peer none of whose actors reported in the round changed no word (and sent none:
+            // k_shard_done_out skips such a round)
+            if (q == x.rank || !x.in[q].done || x.in[q].hdr->newly == 0ull) continue;
             const uint32_t w0 = x.abnd[q] >> 5, nw = ((x.abnd[q + 1] - 1u) >> 5) - w0 + 1u;
             for (uint32_t i = gtid; i < nw; i += gstride) {
                 const uint32_t w = w0 + i, val = x.in[q].done[i], old = a.dbits[w];
@@ -1814,6 +1816,10 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
 // Full gossip on shards: this rank's words of the done bitmap (after F(r)) into every peer's chunk.
 __global__ __launch_bounds__(kBlock) void k_shard_done_out(RoundArgs a, Xchg x) {
     if (applied_converged(a)) return;  // block-uniform
+    // none of this rank's actors reported in the round F(r) applied: no word changed, and the
+    // receivers skip the words (its header's count is 0); the early rounds of a run
+    const uint32_t newly = a.r ? wave_sum(*part_slot(a.parts, (long long)a.r - 1, threadIdx.x & 63u)) : 0u;
+    if (!newly) return;  // uniform: every wave sums the same final sub-counters
     const uint32_t w0 = a.lo >> 5, nw = ((a.hi - 1u) >> 5) - w0 + 1u;
     for (uint32_t q = 0; q < x.world; ++q) {
         if (q == x.rank || !x.out[q].done) continue;
