@@ -687,7 +687,10 @@ constexpr int64_t kTimeEvery = 8;  // kernel timing: one round in 8
 // Kernel timing without a pass after the round kernel: one event pair per group of kTimeGroup
 // consecutive rounds.  Each record stalls the queue: groups of 8 added 9.3 ms to a 129 ms C3
 // run (7%, and 40% of a 20 us tail round); groups of 64 add about 1/8 of that (round 3).
-constexpr int64_t kTimeGroup = 64;
+#ifndef GP_TIME_GROUP
+#define GP_TIME_GROUP 256  // = the largest batch: one event pair per batch (round 4; 64 before)
+#endif
+constexpr int64_t kTimeGroup = GP_TIME_GROUP;
 #ifndef GP_TAIL_BATCH
 #define GP_TAIL_BATCH 32
 #endif
