@@ -694,7 +694,8 @@ constexpr int64_t kTimeGroup = GP_TIME_GROUP;
 #ifndef GP_TAIL_BATCH
 #define GP_TAIL_BATCH 32
 #endif
-constexpr int64_t kTailBatch = GP_TAIL_BATCH;  // rounds per batch in a run's tail (0: no tail rule)
+constexpr int64_t kTailBatch = GP_TAIL_BATCH;
+constexpr int64_t kMaxBatch = 256;  // rounds per gp_step batch at most  // rounds per batch in a run's tail (0: no tail rule)
 
 int ensure_events(Handle* h, int64_t rounds) {
     const size_t need = (size_t)(3 * rounds);
@@ -837,9 +838,9 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         // completed no node doubles again (a long quiet tail, e.g. line gossip, would otherwise
         // pay a host sync every GP_TAIL_BATCH rounds).
         const bool tail = kTailBatch > 0 && h->completed * 32 >= h->lay.nodes * 31;
-        if (!tail) h->batch = std::min<int64_t>(h->batch * 2, 256);
+        if (!tail) h->batch = std::min<int64_t>(h->batch * 2, kMaxBatch);
         else if (!was_tail || h->completed != before) h->batch = kTailBatch;
-        else h->batch = std::min<int64_t>(h->batch * 2, 256);
+        else h->batch = std::min<int64_t>(h->batch * 2, kMaxBatch);
     }
     HIP_TRY(hipEventRecord(h->ev_b, h->stream));
     HIP_TRY(hipEventSynchronize(h->ev_b));
@@ -1519,8 +1520,21 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
     if (g.has_link && (rc = build_links(h))) return bail(rc);
     if (h->sharded && (rc = build_plan(h))) return bail(rc);
     if ((rc = h->alloc(&h->parts, (size_t)kPartRing * kParts * kPartStride))) return bail(rc);
-    if ((rc = ensure_trace(h, 4096))) return bail(rc);
+    // Set up here what gp_step would otherwise allocate inside the timed round loop of a first run
+    // (pinned host memory and device reallocations cost 0.1-1 ms each: `1000 full gossip` ran in
+    // 1.9 ms the first time and 0.28 ms after, tools/first_run_cost.py): the per-round count
+    // array for 2^17 rounds (1 MB; `100000 3D push-sum` takes 62125) and the host-mapped batch
+    // trace for the largest batch.
+    if ((rc = ensure_trace(h, 1 << 17))) return bail(rc);
+    if (hipHostMalloc((void**)&h->h_trace, (size_t)kMaxBatch * sizeof(unsigned long long),
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&h->d_trace, h->h_trace, 0) != hipSuccess)
+        return bail(fail(GP_ENOMEM, "hipHostMalloc of the batch trace failed"));
+    h->h_trace_cap = kMaxBatch;
     if ((rc = reset(h))) return bail(rc);
+    // the code object is loaded at the first kernel launch; a reset without kernels of this library
+    // (full gossip) would leave that to the first timed round (C1 ran in 1.48 instead of 0.29 ms)
+    if (launch_load(h->stream)) return bail(fail(GP_EHIP, "loading the kernels failed"));
     h->lay.device_bytes = (int64_t)h->dev_bytes;
     if (out) *out = h->lay;
     if (shard) {

@@ -272,6 +272,7 @@ void launch_lpos_lists(const uint32_t* off, const uint32_t* list, uint32_t nt, c
 size_t scan_scratch_words(uint32_t n);
 void launch_exclusive_scan(const uint32_t* in, uint32_t* off, uint32_t n, uint32_t* scratch, hipStream_t s);
 void launch_fill_u8(uint8_t* p, uint8_t v, size_t n, hipStream_t s);
+int launch_load(hipStream_t s);  // load the code object now (an empty kernel, synchronised): 0 ok
 // total[a] = total[a-1] + sum of the round-a sub-counters (after the last kernel of a batch)
 // (out: also total[first .. a] into out[], e.g. host-mapped memory)
 void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hipStream_t s,
