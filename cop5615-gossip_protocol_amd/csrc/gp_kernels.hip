@@ -1548,6 +1548,38 @@ __device__ __forceinline__ uint32_t tally_chains(const GsTally& t, uint32_t r) {
     return wave_sum(*part_slot(t.chains, r, threadIdx.x & 63u));
 }
 
+// The receipts of round r - 1 into the counts and states of actors v0 .. v0+3 (program.fs:97-105; a
+// done actor ignores them): returns the new state bytes; the actors that report now are added to
+// done4 (bit j) and newly.  zero: clear the consumed receipt words (round r + 1 adds into them).
+__device__ __forceinline__ uint32_t gs_apply4(const RoundArgs& a, uint32_t v0, uint32_t st4, const uint32_t (&inc)[4],
+                                              bool zero, uint32_t& done4, uint32_t& newly) {
+    if (zero) *reinterpret_cast<uint4*>(a.inc_prev + v0) = make_uint4(0u, 0u, 0u, 0u);
+    uint4 c4 = *reinterpret_cast<const uint4*>(a.cnt + v0);
+    uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
+    const uint32_t st0 = st4;
+    bool counted = false;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t st = (st4 >> (8u * j)) & 0xFFu;
+        uint32_t tok = st & 3u, done = (st >> 2) & 1u;
+        if (inc[j] && !done) {
+            counted = true;
+            const uint32_t c0 = c[j], c1 = c0 + inc[j];
+            c[j] = c1;
+            if (c0 == 0) ++tok;                              // program.fs:99-100
+            if (c0 <= a.threshold && c1 > a.threshold) {     // program.fs:102-104
+                done = 1;
+                ++newly;
+                done4 |= 1u << j;
+            }
+            st4 = (st4 & ~(0xFFu << (8u * j))) | ((tok | (done << 2)) << (8u * j));
+        }
+    }
+    if (counted) *reinterpret_cast<uint4*>(a.cnt + v0) = make_uint4(c[0], c[1], c[2], c[3]);
+    if (st4 != st0) *reinterpret_cast<uint32_t*>(a.gstate + v0) = st4;
+    return st4;
+}
+
 __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
     extern __shared__ uint32_t tcnt[];  // tally rounds: receipts per target bucket (t.nb)
     const uint32_t r = a.r;
@@ -1603,33 +1635,9 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
                 if (v0 + j >= na) inc[j] = 0u;  // the padding past the last actor
-            if (inc[0] | inc[1] | inc[2] | inc[3]) {
+            if (inc[0] | inc[1] | inc[2] | inc[3])
                 // consumed; round r + 1 adds its receipts here (a tallied round writes them whole)
-                if (!tally_next) *reinterpret_cast<uint4*>(a.inc_prev + v0) = make_uint4(0u, 0u, 0u, 0u);
-                uint4 c4 = *reinterpret_cast<const uint4*>(a.cnt + v0);
-                uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
-                const uint32_t st0 = st4;
-                bool counted = false;
-#pragma unroll
-                for (uint32_t j = 0; j < 4; ++j) {
-                    const uint32_t st = (st4 >> (8u * j)) & 0xFFu;
-                    uint32_t tok = st & 3u, done = (st >> 2) & 1u;
-                    if (inc[j] && !done) {
-                        counted = true;
-                        const uint32_t c0 = c[j], c1 = c0 + inc[j];
-                        c[j] = c1;
-                        if (c0 == 0) ++tok;                              // program.fs:99-100
-                        if (c0 <= a.threshold && c1 > a.threshold) {     // program.fs:102-104
-                            done = 1;
-                            ++newly;
-                            done4 |= 1u << j;
-                        }
-                        st4 = (st4 & ~(0xFFu << (8u * j))) | ((tok | (done << 2)) << (8u * j));
-                    }
-                }
-                if (counted) *reinterpret_cast<uint4*>(a.cnt + v0) = make_uint4(c[0], c[1], c[2], c[3]);
-                if (st4 != st0) *reinterpret_cast<uint32_t*>(a.gstate + v0) = st4;
-            }
+                st4 = gs_apply4(a, v0, st4, inc, !tally_next, done4, newly);
             // emit round r: one draw per activation chain (program.fs:89-95)
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j) {
@@ -1724,32 +1732,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
                 if (!((mine >> j) & 1u)) inc[j] = 0u;  // another rank's actor (or padding)
-            if (inc[0] | inc[1] | inc[2] | inc[3]) {
-                *reinterpret_cast<uint4*>(a.inc_prev + v0) = make_uint4(0u, 0u, 0u, 0u);
-                uint4 c4 = *reinterpret_cast<const uint4*>(a.cnt + v0);
-                uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
-                const uint32_t st0 = st4;
-                bool counted = false;
-#pragma unroll
-                for (uint32_t j = 0; j < 4; ++j) {
-                    const uint32_t st = (st4 >> (8u * j)) & 0xFFu;
-                    uint32_t tok = st & 3u, done = (st >> 2) & 1u;
-                    if (inc[j] && !done) {
-                        counted = true;
-                        const uint32_t c0 = c[j], c1 = c0 + inc[j];
-                        c[j] = c1;
-                        if (c0 == 0) ++tok;                              // program.fs:99-100
-                        if (c0 <= a.threshold && c1 > a.threshold) {     // program.fs:102-104
-                            done = 1;
-                            ++newly;
-                            done4 |= 1u << j;
-                        }
-                        st4 = (st4 & ~(0xFFu << (8u * j))) | ((tok | (done << 2)) << (8u * j));
-                    }
-                }
-                if (counted) *reinterpret_cast<uint4*>(a.cnt + v0) = make_uint4(c[0], c[1], c[2], c[3]);
-                if (st4 != st0) *reinterpret_cast<uint32_t*>(a.gstate + v0) = st4;
-            }
+            if (inc[0] | inc[1] | inc[2] | inc[3]) st4 = gs_apply4(a, v0, st4, inc, true, done4, newly);
         }
         // emit round r: one draw per activation chain (program.fs:89-95); local receipts now, remote
         // ones after the block's reservation
