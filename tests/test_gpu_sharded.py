@@ -252,7 +252,7 @@ def test_shards_activity_tiers_default():
         e.close()
 
 
-@pytest.mark.parametrize("n,world,seed", [(1000, 2, 1), (20000, 3, 4), (100000, 5, 2), (300000, 8, 6)])
+@pytest.mark.parametrize("n,world,seed", [(1000, 2, 1), (20000, 3, 4), (100000, 5, 2), (300000, 8, 6), (2000000, 8, 3)])
 def test_full_gossip_tight_tiers_vs_oracle(n, world, seed):
     """Full gossip on shards with tight activity tiers: the senders filter remote receipts on the
     replicated done bitmap, the chunks shrink with the receipts still sent, overflowed batches are
