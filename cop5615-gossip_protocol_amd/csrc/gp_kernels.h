@@ -1,5 +1,6 @@
 // gp_kernels.h — parameter blocks and launchers of the gfx950 round kernels (gp_kernels.hip).
 #pragma once
+#include <type_traits>
 #include "gp_common.h"
 
 namespace gp {
@@ -220,6 +221,10 @@ void launch_gs_push(const RoundArgs& a, const Launch& l);
 // scatter of the receipts by bucket (the draws recomputed) and an LDS tally per bucket then write
 // inc_cur whole.  Receipts to done targets are not filtered there (the receiver drops them).
 constexpr uint32_t kTallyShift = 15;          // 32768 targets per bucket: 128 KB of LDS counters
+#ifndef GP_TALLY_U16
+#define GP_TALLY_U16 1
+#endif
+typedef std::conditional<GP_TALLY_U16 != 0, uint16_t, uint32_t>::type TallyTarget;
 constexpr uint32_t kMaxTallyBuckets = 4096;   // k_gs_full4's LDS counters: 16 KB at most
 #ifndef GP_TALLY_LATE_DIV
 #define GP_TALLY_LATE_DIV 64  // A/B knob; 0: no late tally
@@ -228,7 +233,8 @@ constexpr uint64_t kTallyLateDiv = GP_TALLY_LATE_DIV;  // also tally (filter on)
 struct GsTally {
     uint32_t* cnt;     // [nb * W] receipts per (bucket, workgroup), bucket-major; null: no tally
     uint32_t* off;     // [nb * W + 1] exclusive scan of cnt
-    uint32_t* tgt;     // receipts grouped by bucket (2 per actor at most)
+    TallyTarget* tgt;  // receipts grouped by bucket (2 per actor at most): the target's offset in
+                       // its bucket (16 bits: 32768 targets per bucket; A/B knob GP_TALLY_U16)
     uint32_t* scratch; // scan scratch (scan_scratch_words(nb * W))
     uint32_t* chains;  // [4][kParts * kPartStride]: chains emitted in round r, ring slot r & 3
     uint32_t* on;      // [4]: round r tallies (written by block 0 of F(r))

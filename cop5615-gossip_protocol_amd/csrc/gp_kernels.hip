@@ -1838,11 +1838,11 @@ __global__ __launch_bounds__(kBlock) void k_gs_tally_scatter(RoundArgs a, GsTall
                 const uint4 px = philox(v, r, kStreamGossip, a.seed);
                 const uint32_t t0 = scale_draw(px.x, a.nodes), u0 = t0 + (t0 >= v ? 1u : 0u);
                 const uint32_t b0 = u0 >> kTallyShift;
-                t.tgt[atomicAdd(&tpos[b0], 1u)] = u0;
+                t.tgt[atomicAdd(&tpos[b0], 1u)] = (TallyTarget)(u0 & ((1u << kTallyShift) - 1u));
                 if (tok > 1) {
                     const uint32_t t1 = scale_draw(px.y, a.nodes), u1 = t1 + (t1 >= v ? 1u : 0u);
                     const uint32_t b1 = u1 >> kTallyShift;
-                    t.tgt[atomicAdd(&tpos[b1], 1u)] = u1;
+                    t.tgt[atomicAdd(&tpos[b1], 1u)] = (TallyTarget)(u1 & ((1u << kTallyShift) - 1u));
                 }
             }
         }
@@ -1962,7 +1962,7 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
         __syncthreads();
         for (uint32_t i = tid; i < total; i += kScatBlock) {  // hs[b] now ends bucket b's run
             const uint32_t u = S[i], b = u >> kTallyShift;
-            t.tgt[tpos[b] + i - (b ? hs[b - 1u] : 0u)] = u;
+            t.tgt[tpos[b] + i - (b ? hs[b - 1u] : 0u)] = (TallyTarget)(u & ((1u << kTallyShift) - 1u));
         }
         __syncthreads();
         for (uint32_t b = tid; b < nb; b += kScatBlock) tpos[b] += hs[b] - (b ? hs[b - 1u] : 0u);
@@ -1986,7 +1986,7 @@ __global__ __launch_bounds__(kCountBlock) void k_gs_tally_count(RoundArgs a, GsT
     __syncthreads();
     const uint32_t b = blockIdx.x;
     const uint32_t s0 = t.off[b * t.W], s1 = t.off[(b + 1u) * t.W];
-    for (uint32_t i = s0 + threadIdx.x; i < s1; i += kCountBlock) atomicAdd(&h[t.tgt[i] & (S - 1u)], 1u);
+    for (uint32_t i = s0 + threadIdx.x; i < s1; i += kCountBlock) atomicAdd(&h[(uint32_t)t.tgt[i] & (S - 1u)], 1u);
     __syncthreads();
     const uint32_t base = b << kTallyShift, na = a.hi;
     const uint32_t n = na - base < S ? na - base : S;
