@@ -1548,6 +1548,28 @@ __device__ __forceinline__ uint32_t tally_chains(const GsTally& t, uint32_t r) {
     return wave_sum(*part_slot(t.chains, r, threadIdx.x & 63u));
 }
 
+// The state bytes (st4) and the round r - 1 receipt words of actors v0 .. v0+3.  Deep in a run's
+// tail (deep: block-uniform) a quad of four done actors skips its receipt words: a done actor ignores
+// receipts (program.fs:92), so its words are neither read nor cleared, and whatever lands in them
+// later is ignored too (the tally's count pass rewrites them whole); elsewhere both loads go out
+// together.
+#ifndef GP_DEEP_DIV
+#define GP_DEEP_DIV 64  // A/B knob: "deep" = fewer than 1/GP_DEEP_DIV of the nodes not done (0: off)
+#endif
+__device__ __forceinline__ uint4 load_quad(const RoundArgs& a, uint32_t v0, uint32_t r, bool deep, uint32_t& st4) {
+    uint4 in4 = make_uint4(0u, 0u, 0u, 0u);
+    st4 = *reinterpret_cast<const uint32_t*>(a.gstate + v0);
+    if (deep) {
+        if (r && (st4 & 0x04040404u) != 0x04040404u) in4 = *reinterpret_cast<const uint4*>(a.inc_prev + v0);
+    } else if (r) {
+        in4 = *reinterpret_cast<const uint4*>(a.inc_prev + v0);
+    }
+    return in4;
+}
+__device__ __forceinline__ bool deep_tail(unsigned long long prev, uint32_t target) {
+    return GP_DEEP_DIV > 0 && prev < target && (unsigned long long)(target - prev) * GP_DEEP_DIV < target;
+}
+
 // The receipts of round r - 1 into the counts and states of actors v0 .. v0+3 (program.fs:97-105; a
 // done actor ignores them): returns the new state bytes; the actors that report now are added to
 // done4 (bit j) and newly.  zero: clear the consumed receipt words (round r + 1 adds into them).
@@ -1616,6 +1638,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
         __syncthreads();
     }
     const bool filter = (unsigned long long)GP_GS_FILTER_DIV * prev >= a.target;
+    const bool deep = deep_tail(prev, a.target);
     const uint32_t na = a.hi;  // one GPU: actors [0, na)
     const uint32_t nq = (na + 3u) >> 2;
     const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;
@@ -1628,9 +1651,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
         const uint32_t v0 = q << 2;
         uint32_t st4 = 0, done4 = 0;
         if (valid) {
-            st4 = *reinterpret_cast<const uint32_t*>(a.gstate + v0);
-            uint4 in4 = make_uint4(0u, 0u, 0u, 0u);
-            if (r) in4 = *reinterpret_cast<const uint4*>(a.inc_prev + v0);
+            uint4 in4 = load_quad(a, v0, r, deep, st4);
             uint32_t inc[4] = {in4.x, in4.y, in4.z, in4.w};
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
@@ -1710,6 +1731,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
     if (r) prev = gate_count(a, (long long)r - 1);
     if (r && prev >= a.target) return;
     const bool filter = (unsigned long long)GP_GS_FILTER_DIV * prev >= a.target;  // global count
+    const bool deep = deep_tail(prev, a.target);
     const uint32_t lo = a.lo, hi = a.hi;
     // quads from a multiple of 8 (8 lanes = 32 actors = one bitmap word)
     const uint32_t q0 = (lo >> 2) & ~7u, q1 = (hi + 3u) >> 2, nq = q1 - q0;
@@ -1725,9 +1747,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) mine |= (valid && v0 + j - lo < hi - lo) ? 1u << j : 0u;
         if (mine) {
-            st4 = *reinterpret_cast<const uint32_t*>(a.gstate + v0);
-            uint4 in4 = make_uint4(0u, 0u, 0u, 0u);
-            if (r) in4 = *reinterpret_cast<const uint4*>(a.inc_prev + v0);
+            uint4 in4 = load_quad(a, v0, r, deep, st4);
             uint32_t inc[4] = {in4.x, in4.y, in4.z, in4.w};
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
