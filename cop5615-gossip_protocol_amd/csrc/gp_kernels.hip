@@ -1910,7 +1910,8 @@ __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t x, uint32_t* wsum
 
 // Tallied round, batched placement: a workgroup of kScatK x 256 threads walks the actors of
 // k_gs_full4's workgroups kScatK*s .. kScatK*s + kScatK - 1 (their segments of every bucket are
-// adjacent, so it fills them as one), in batches of as many walk iterations as its LDS holds.  A
+// adjacent, so it fills them as one; its start in each is the bucket's start, scanned here from
+// k_tally_rows' row totals, plus that row's prefix), in batches of as many walk iterations as its LDS holds.  A
 // batch is drawn twice: once to count its receipts per bucket, once to sort them by bucket in LDS;
 // then consecutive lanes store consecutive receipts of a bucket.  k_gs_tally_scatter stores each
 // receipt where its LDS position falls, one 4-byte store per line: its 98M receipts per C4 peak
@@ -1927,7 +1928,29 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
     uint32_t* hs = lds + nb;          // batch counts -> starts -> ends per bucket
     uint32_t* misc = lds + 2u * nb;   // [0]: batch total; [16, 32): scan wave sums
     uint32_t* S = misc + 32;          // the batch's receipts, bucket-sorted
-    for (uint32_t i = tid; i < nb; i += kScatBlock) tpos[i] = t.off[i * W + kScatK * blockIdx.x];
+    {  // bucket starts: exclusive scan of k_tally_rows' row totals, 4 buckets per thread
+        const uint32_t G = W / kScatK;
+        const uint32_t* tot = t.off + (size_t)nb * G;
+        uint32_t* bst = t.off + (size_t)nb * G + nb;  // for k_gs_tally_count (workgroup 0 stores it)
+        uint32_t v[4], s = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t b = 4u * tid + j;
+            v[j] = b < nb ? tot[b] : 0u;
+            s += v[j];
+        }
+        uint32_t run = block_excl_scan_n<kScatBlock>(s, misc + 16);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t b = 4u * tid + j;
+            if (b < nb) {
+                tpos[b] = run + t.off[(size_t)b * G + blockIdx.x];
+                if (blockIdx.x == 0) bst[b] = run;
+            }
+            run += v[j];
+        }
+        if (blockIdx.x == 0 && tid == kScatBlock - 1u) bst[nb] = run;  // the last thread ends at the total
+    }
     // this thread's walk: node_range of k_gs_full4 workgroup w, thread lt
     const uint32_t w = kScatK * blockIdx.x + (tid >> 8), lt = tid & (kBlock - 1u);
     const uint32_t na = a.hi, nq = (na + 3u) >> 2;
@@ -1998,14 +2021,15 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
 #define GP_COUNT_BLOCK 1024
 #endif
 constexpr uint32_t kCountBlock = GP_COUNT_BLOCK;
-__global__ __launch_bounds__(kCountBlock) void k_gs_tally_count(RoundArgs a, GsTally t) {
+__global__ __launch_bounds__(kCountBlock) void k_gs_tally_count(RoundArgs a, GsTally t, const uint32_t* bst) {
     extern __shared__ uint32_t h[];
     if (!t.on[a.r & 3u]) return;  // uniform
     constexpr uint32_t S = 1u << kTallyShift;
     for (uint32_t i = threadIdx.x; i < S; i += kCountBlock) h[i] = 0u;
     __syncthreads();
     const uint32_t b = blockIdx.x;
-    const uint32_t s0 = t.off[b * t.W], s1 = t.off[(b + 1u) * t.W];
+    // bucket starts: k_gs_tally_scatter_lds's (bst) or the full scan's
+    const uint32_t s0 = bst ? bst[b] : t.off[b * t.W], s1 = bst ? bst[b + 1u] : t.off[(b + 1u) * t.W];
     for (uint32_t i = s0 + threadIdx.x; i < s1; i += kCountBlock) atomicAdd(&h[(uint32_t)t.tgt[i] & (S - 1u)], 1u);
     __syncthreads();
     const uint32_t base = b << kTallyShift, na = a.hi;
@@ -2207,6 +2231,38 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(const uint32_t* in, uint3
     }
 }
 
+// Tallied round, batched placement: the part of the scan k_gs_tally_scatter_lds reads.  One
+// workgroup per bucket row of cnt stores the row's prefix at each scatter workgroup's first column
+// (off[b * G + s], G = W / kScatK) and the row total (off[nb * G + b]); the scatter workgroups scan
+// the nb totals themselves.  One pass reading cnt once, in place of the reduce / top / apply scan
+// of all nb * W counts (two reads and a whole write of cnt, profiles/round4/tally_rows).
+constexpr uint32_t kRowP = ((uint32_t)kMaxGrid / kScatK + kBlock - 1u) / kBlock;
+__global__ __launch_bounds__(kBlock) void k_tally_rows(GsTally t, const uint32_t* gate) {
+    if (!*gate) return;
+    const uint32_t b = blockIdx.x, G = t.W / kScatK, P = (G + kBlock - 1u) / kBlock;
+    const uint4* row = reinterpret_cast<const uint4*>(t.cnt + (size_t)b * t.W);
+    const uint32_t g0 = threadIdx.x * P;
+    uint32_t v[kRowP], s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kRowP; ++j) {
+        v[j] = 0u;
+        if (j < P && g0 + j < G) {
+            const uint4 q = row[g0 + j];
+            v[j] = q.x + q.y + q.z + q.w;
+        }
+        s += v[j];
+    }
+    uint32_t total;
+    uint32_t run = block_excl_scan(s, total);
+    uint32_t* o = t.off + (size_t)b * G;
+#pragma unroll
+    for (uint32_t j = 0; j < kRowP; ++j) {
+        if (j < P && g0 + j < G) o[g0 + j] = run;
+        run += v[j];
+    }
+    if (threadIdx.x == 0) t.off[(size_t)t.nb * G + b] = total;
+}
+
 __global__ void k_fill_u8(uint8_t* p, uint8_t val, size_t n) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         p[i] = val;
@@ -2363,17 +2419,22 @@ int prepare_gs_tally() {
 void launch_gs_tally(const RoundArgs& a, const GsTally& t, const Launch& l) {
     if (!t.cnt || !a.r) return;
     const uint32_t* gate = t.on + (a.r & 3u);
-    const uint32_t n = t.nb * t.W, nb = (n + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kBlock), 0, l.stream, t.cnt, n, t.scratch, gate);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, l.stream, t.scratch, nb, gate);
-    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kBlock), 0, l.stream, t.cnt, t.off, n, t.scratch, gate);
     const uint32_t cap = kScatLdsBytes / 4u - 2u * t.nb - 32u;
-    if (g_scatter_lds && t.W % kScatK == 0 && t.nb <= 4u * kScatBlock && cap >= kScatMaxPerIter)
+    const uint32_t* bst = nullptr;
+    if (g_scatter_lds && t.W % kScatK == 0 && t.W <= (uint32_t)kMaxGrid && t.nb <= 4u * kScatBlock &&
+        cap >= kScatMaxPerIter) {
+        hipLaunchKernelGGL(k_tally_rows, dim3(t.nb), dim3(kBlock), 0, l.stream, t, gate);
         hipLaunchKernelGGL(k_gs_tally_scatter_lds, dim3(t.W / kScatK), dim3(kScatBlock), kScatLdsBytes, l.stream, a, t, cap);
-    else
+        bst = t.off + (size_t)t.nb * (t.W / kScatK) + t.nb;
+    } else {
+        const uint32_t n = t.nb * t.W, nb = (n + kScanTile - 1) / kScanTile;
+        hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kBlock), 0, l.stream, t.cnt, n, t.scratch, gate);
+        hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, l.stream, t.scratch, nb, gate);
+        hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kBlock), 0, l.stream, t.cnt, t.off, n, t.scratch, gate);
         hipLaunchKernelGGL(k_gs_tally_scatter, dim3(t.W), dim3(kBlock), t.nb * (unsigned)sizeof(uint32_t), l.stream, a, t);
+    }
     hipLaunchKernelGGL(k_gs_tally_count, dim3(t.nb), dim3(kCountBlock), (1u << kTallyShift) * (unsigned)sizeof(uint32_t),
-                       l.stream, a, t);
+                       l.stream, a, t, bst);
 }
 
 void launch_gs_push(const RoundArgs& a, const Launch& l) {

@@ -4,7 +4,7 @@ set -o pipefail
 R="$GRAFT_REPO_ROOT"; cd "$R"
 O="$R/gpurun_out/${OUT:-r4_c4final}"; mkdir -p "$O"
 PMC_WORKLOAD="100000000 full gossip" PMC_GROUP="k_gs_full4+tally" PMC_ROUNDS=69 \
-  PMC_KERNELS="k_gs_full4,k_scan_reduce,k_scan_top,k_scan_apply,k_gs_tally_scatter_lds,k_gs_tally_count" \
+  PMC_KERNELS="${PMC_KERNELS:-k_gs_full4,k_tally_rows,k_gs_tally_scatter_lds,k_gs_tally_count}" \
   PROF_ARGS="--n 100000000 --topology full --algorithm gossip" OUT=${OUT:-r4_c4final}_pmc bash tools/gpu.sh pmcgroup || exit 1
 cp "$R/gpurun_out/${OUT:-r4_c4final}_pmc/pmc_group.json" "$O/pmc_group.json"
 timeout -k 10 240 python3 bench.py --workload c4 --steps 5 --warmup 1 > "$O/c4_bench.json" 2> "$O/c4_bench.err" || { tail "$O/c4_bench.err"; exit 1; }
