@@ -1890,7 +1890,7 @@ __device__ __forceinline__ void gs_draws4(const RoundArgs& a, uint32_t r, uint32
 
 // Exclusive scan of one u32 per thread over a workgroup of NT threads (wsum: NT / 64 words).
 template <uint32_t NT>
-__device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t x, uint32_t* wsum) {
+__device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t x, uint32_t* wsum, uint32_t* total = nullptr) {
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t inc = x;
 #pragma unroll
@@ -1900,22 +1900,31 @@ __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t x, uint32_t* wsum
     }
     if (lane == 63) wsum[w] = inc;
     __syncthreads();
-    uint32_t base = 0;
+    uint32_t base = 0, all = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < NT / 64; ++i)
+    for (uint32_t i = 0; i < NT / 64; ++i) {
         if (i < w) base += wsum[i];
+        all += wsum[i];
+    }
     __syncthreads();
+    if (total) *total = all;
     return base + inc - x;
 }
 
-// Tallied round, batched placement: a workgroup of kScatK x 256 threads walks the actors of
-// k_gs_full4's workgroups kScatK*s .. kScatK*s + kScatK - 1 (their segments of every bucket are
-// adjacent, so it fills them as one; its start in each is the bucket's start, scanned here from
-// k_tally_rows' row totals, plus that row's prefix), in batches of as many walk iterations as its LDS holds.  A
-// batch is drawn twice: once to count its receipts per bucket, once to sort them by bucket in LDS;
-// then consecutive lanes store consecutive receipts of a bucket.  k_gs_tally_scatter stores each
+// Tallied round, batched placement: a workgroup of kScatK x 256 threads places the receipts of
+// k_gs_full4's workgroups kScatK*s .. kScatK*s + kScatK - 1, one after another (their segments of
+// every bucket are adjacent; the first starts at the bucket's start, scanned here from
+// k_tally_rows' row totals, plus that row's prefix).  k_gs_full4 counted each workgroup's receipts
+// per bucket (cnt), so when they fit in LDS their bucket starts in LDS are known and the draws are
+// made once: each receipt goes to its bucket's run in LDS, then consecutive lanes store
+// consecutive receipts of a bucket.  A workgroup with more receipts than LDS holds is placed in
+// batches of walk iterations, each drawn twice (count, then sort).  The walk of one k_gs_full4
+// workgroup is dealt round-robin to the kScatK thread groups.  k_gs_tally_scatter stores each
 // receipt where its LDS position falls, one 4-byte store per line: its 98M receipts per C4 peak
 // round wrote 2.94 GB (7.5x the receipt bytes, profiles/round3/c4_tally/pmc_scatter.txt).
+#ifndef GP_SCAT_ONEPASS
+#define GP_SCAT_ONEPASS 1  // A/B and test knob; 0: every workgroup in counted batches
+#endif
 constexpr uint32_t kScatK = 4;
 constexpr uint32_t kScatBlock = kScatK * kBlock;
 constexpr uint32_t kScatMaxPerIter = kScatBlock * 8u;  // 4 actors x 2 chains per thread
@@ -1928,6 +1937,7 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
     uint32_t* hs = lds + nb;          // batch counts -> starts -> ends per bucket
     uint32_t* misc = lds + 2u * nb;   // [0]: batch total; [16, 32): scan wave sums
     uint32_t* S = misc + 32;          // the batch's receipts, bucket-sorted
+    uint4 cw[4];  // receipts of buckets 4 * tid + j from workgroups kScatK*s + 0..3 (x..w)
     {  // bucket starts: exclusive scan of k_tally_rows' row totals, 4 buckets per thread
         const uint32_t G = W / kScatK;
         const uint32_t* tot = t.off + (size_t)nb * G;
@@ -1937,6 +1947,8 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
         for (uint32_t j = 0; j < 4; ++j) {
             const uint32_t b = 4u * tid + j;
             v[j] = b < nb ? tot[b] : 0u;
+            cw[j] = b < nb ? *reinterpret_cast<const uint4*>(t.cnt + (size_t)b * W + kScatK * blockIdx.x)
+                           : make_uint4(0u, 0u, 0u, 0u);
             s += v[j];
         }
         uint32_t run = block_excl_scan_n<kScatBlock>(s, misc + 16);
@@ -1951,66 +1963,100 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
         }
         if (blockIdx.x == 0 && tid == kScatBlock - 1u) bst[nb] = run;  // the last thread ends at the total
     }
-    // this thread's walk: node_range of k_gs_full4 workgroup w, thread lt
-    const uint32_t w = kScatK * blockIdx.x + (tid >> 8), lt = tid & (kBlock - 1u);
-    const uint32_t na = a.hi, nq = (na + 3u) >> 2;
-    const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;
-    const uint32_t base = (w & 7u) * span4, step = (W >> 3) * kBlock;
-    const uint32_t end = base >= nq ? 0u : (base + span4 < nq ? base + span4 : nq);
-    const uint32_t q0 = base + (w >> 3) * kBlock + lt;
-    const uint32_t iters = (span4 + step - 1u) / step;
-    for (uint32_t it = 0; it < iters;) {  // uniform
-        for (uint32_t i = tid; i < nb; i += kScatBlock) hs[i] = 0u;
-        if (tid == 0) misc[0] = 0u;
-        __syncthreads();
-        uint32_t it1 = it, total = 0;
-        do {  // count: add iterations while one more cannot overflow S
-            const uint32_t q = q0 + it1 * step;
-            uint32_t c = 0;
-            if (q < end)
-                gs_draws4(a, r, q << 2, *reinterpret_cast<const uint32_t*>(a.gstate + (q << 2)), na, [&](uint32_t u) {
-                    atomicAdd(&hs[u >> kTallyShift], 1u);
-                    ++c;
-                });
-            c = wave_sum(c);
-            if ((tid & 63u) == 0) atomicAdd(&misc[0], c);
-            ++it1;
-            __syncthreads();
-            total = misc[0];
-            __syncthreads();
-        } while (it1 < iters && total + kScatMaxPerIter <= cap);
-        {  // starts: exclusive scan of the counts, 4 buckets per thread (nb <= 4 * kScatBlock)
-            uint32_t v[4], s = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                const uint32_t b = 4u * tid + j;
-                v[j] = b < nb ? hs[b] : 0u;
-                s += v[j];
-            }
-            uint32_t run = block_excl_scan_n<kScatBlock>(s, misc + 16);
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                const uint32_t b = 4u * tid + j;
-                if (b < nb) hs[b] = run;
-                run += v[j];
-            }
-        }
-        __syncthreads();
-        for (uint32_t i = it; i < it1; ++i) {  // sort: the same draws, placed by bucket
-            const uint32_t q = q0 + i * step;
-            if (q < end)
-                gs_draws4(a, r, q << 2, *reinterpret_cast<const uint32_t*>(a.gstate + (q << 2)), na,
-                          [&](uint32_t u) { S[atomicAdd(&hs[u >> kTallyShift], 1u)] = u; });
-        }
-        __syncthreads();
-        for (uint32_t i = tid; i < total; i += kScatBlock) {  // hs[b] now ends bucket b's run
+    // stores a sorted batch of `total` receipts (hs[b]: the end of bucket b's run) and advances tpos
+    auto place = [&](uint32_t total) {
+        for (uint32_t i = tid; i < total; i += kScatBlock) {
             const uint32_t u = S[i], b = u >> kTallyShift;
             t.tgt[tpos[b] + i - (b ? hs[b - 1u] : 0u)] = (TallyTarget)(u & ((1u << kTallyShift) - 1u));
         }
         __syncthreads();
         for (uint32_t b = tid; b < nb; b += kScatBlock) tpos[b] += hs[b] - (b ? hs[b - 1u] : 0u);
         __syncthreads();
-        it = it1;
+    };
+    const uint32_t lt = tid & (kBlock - 1u), g = tid >> 8;
+    const uint32_t na = a.hi, nq = (na + 3u) >> 2;
+    const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;
+    const uint32_t step = (W >> 3) * kBlock;
+    const uint32_t iters = (span4 + step - 1u) / step, sup = (iters + kScatK - 1u) / kScatK;
+    for (uint32_t k = 0; k < kScatK; ++k) {  // uniform
+        // k_gs_full4 workgroup w's walk (node_range, thread lt): its iteration kScatK * i + g is
+        // this thread's i-th
+        const uint32_t w = kScatK * blockIdx.x + k;
+        const uint32_t base = (w & 7u) * span4;
+        const uint32_t end = base >= nq ? 0u : (base + span4 < nq ? base + span4 : nq);
+        const uint32_t q0 = base + (w >> 3) * kBlock + lt;
+        uint32_t v[4], s = 0, all;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            v[j] = k == 0u ? cw[j].x : k == 1u ? cw[j].y : k == 2u ? cw[j].z : cw[j].w;
+            s += v[j];
+        }
+        uint32_t run = block_excl_scan_n<kScatBlock>(s, misc + 16, &all);
+        if (GP_SCAT_ONEPASS && all <= cap) {  // one pass: starts from the counts
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t b = 4u * tid + j;
+                if (b < nb) hs[b] = run;
+                run += v[j];
+            }
+            __syncthreads();
+            for (uint32_t i = 0; i < sup; ++i) {
+                const uint32_t q = q0 + (kScatK * i + g) * step;
+                if (q < end)
+                    gs_draws4(a, r, q << 2, *reinterpret_cast<const uint32_t*>(a.gstate + (q << 2)), na,
+                              [&](uint32_t u) { S[atomicAdd(&hs[u >> kTallyShift], 1u)] = u; });
+            }
+            __syncthreads();
+            place(all);
+            continue;
+        }
+        for (uint32_t it = 0; it < sup;) {  // counted batches (uniform)
+            for (uint32_t i = tid; i < nb; i += kScatBlock) hs[i] = 0u;
+            if (tid == 0) misc[0] = 0u;
+            __syncthreads();
+            uint32_t it1 = it, total = 0;
+            do {  // count: add iterations while one more cannot overflow S
+                const uint32_t q = q0 + (kScatK * it1 + g) * step;
+                uint32_t c = 0;
+                if (q < end)
+                    gs_draws4(a, r, q << 2, *reinterpret_cast<const uint32_t*>(a.gstate + (q << 2)), na, [&](uint32_t u) {
+                        atomicAdd(&hs[u >> kTallyShift], 1u);
+                        ++c;
+                    });
+                c = wave_sum(c);
+                if ((tid & 63u) == 0) atomicAdd(&misc[0], c);
+                ++it1;
+                __syncthreads();
+                total = misc[0];
+                __syncthreads();
+            } while (it1 < sup && total + kScatMaxPerIter <= cap);
+            {  // starts: exclusive scan of the counts, 4 buckets per thread (nb <= 4 * kScatBlock)
+                uint32_t c[4], cs = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t b = 4u * tid + j;
+                    c[j] = b < nb ? hs[b] : 0u;
+                    cs += c[j];
+                }
+                uint32_t crun = block_excl_scan_n<kScatBlock>(cs, misc + 16);
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t b = 4u * tid + j;
+                    if (b < nb) hs[b] = crun;
+                    crun += c[j];
+                }
+            }
+            __syncthreads();
+            for (uint32_t i = it; i < it1; ++i) {  // sort: the same draws, placed by bucket
+                const uint32_t q = q0 + (kScatK * i + g) * step;
+                if (q < end)
+                    gs_draws4(a, r, q << 2, *reinterpret_cast<const uint32_t*>(a.gstate + (q << 2)), na,
+                              [&](uint32_t u) { S[atomicAdd(&hs[u >> kTallyShift], 1u)] = u; });
+            }
+            __syncthreads();
+            place(total);
+            it = it1;
+        }
     }
 }
 
