@@ -1922,6 +1922,9 @@ __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t x, uint32_t* wsum
 // workgroup is dealt round-robin to the kScatK thread groups.  k_gs_tally_scatter stores each
 // receipt where its LDS position falls, one 4-byte store per line: its 98M receipts per C4 peak
 // round wrote 2.94 GB (7.5x the receipt bytes, profiles/round3/c4_tally/pmc_scatter.txt).
+#ifndef GP_SCAT_XCD
+#define GP_SCAT_XCD 1  // A/B knob; 0: column group = workgroup index
+#endif
 #ifndef GP_SCAT_ONEPASS
 #define GP_SCAT_ONEPASS 1  // A/B and test knob; 0: every workgroup in counted batches
 #endif
@@ -1937,9 +1940,13 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
     uint32_t* hs = lds + nb;          // batch counts -> starts -> ends per bucket
     uint32_t* misc = lds + 2u * nb;   // [0]: batch total; [16, 32): scan wave sums
     uint32_t* S = misc + 32;          // the batch's receipts, bucket-sorted
-    uint4 cw[4];  // receipts of buckets 4 * tid + j from workgroups kScatK*s + 0..3 (x..w)
+    // column group sg: consecutive groups on one XCD (workgroups are dealt round-robin to the 8
+    // XCDs), so the count and prefix lines they read, and the bucket segments they write next to
+    // each other, meet in one L2
+    const uint32_t G = W / kScatK;
+    const uint32_t sg = (GP_SCAT_XCD && (G & 7u) == 0u) ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    uint4 cw[4];  // receipts of buckets 4 * tid + j from workgroups kScatK*sg + 0..3 (x..w)
     {  // bucket starts: exclusive scan of k_tally_rows' row totals, 4 buckets per thread
-        const uint32_t G = W / kScatK;
         const uint32_t* tot = t.off + (size_t)nb * G;
         uint32_t* bst = t.off + (size_t)nb * G + nb;  // for k_gs_tally_count (workgroup 0 stores it)
         uint32_t v[4], s = 0;
@@ -1947,7 +1954,7 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
         for (uint32_t j = 0; j < 4; ++j) {
             const uint32_t b = 4u * tid + j;
             v[j] = b < nb ? tot[b] : 0u;
-            cw[j] = b < nb ? *reinterpret_cast<const uint4*>(t.cnt + (size_t)b * W + kScatK * blockIdx.x)
+            cw[j] = b < nb ? *reinterpret_cast<const uint4*>(t.cnt + (size_t)b * W + kScatK * sg)
                            : make_uint4(0u, 0u, 0u, 0u);
             s += v[j];
         }
@@ -1956,12 +1963,12 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
         for (uint32_t j = 0; j < 4; ++j) {
             const uint32_t b = 4u * tid + j;
             if (b < nb) {
-                tpos[b] = run + t.off[(size_t)b * G + blockIdx.x];
-                if (blockIdx.x == 0) bst[b] = run;
+                tpos[b] = run + t.off[(size_t)b * G + sg];
+                if (sg == 0) bst[b] = run;
             }
             run += v[j];
         }
-        if (blockIdx.x == 0 && tid == kScatBlock - 1u) bst[nb] = run;  // the last thread ends at the total
+        if (sg == 0 && tid == kScatBlock - 1u) bst[nb] = run;  // the last thread ends at the total
     }
     // stores a sorted batch of `total` receipts (hs[b]: the end of bucket b's run) and advances tpos
     auto place = [&](uint32_t total) {
@@ -1981,7 +1988,7 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
     for (uint32_t k = 0; k < kScatK; ++k) {  // uniform
         // k_gs_full4 workgroup w's walk (node_range, thread lt): its iteration kScatK * i + g is
         // this thread's i-th
-        const uint32_t w = kScatK * blockIdx.x + k;
+        const uint32_t w = kScatK * sg + k;
         const uint32_t base = (w & 7u) * span4;
         const uint32_t end = base >= nq ? 0u : (base + span4 < nq ? base + span4 : nq);
         const uint32_t q0 = base + (w >> 3) * kBlock + lt;
