@@ -1548,6 +1548,20 @@ __device__ __forceinline__ uint32_t tally_chains(const GsTally& t, uint32_t r) {
     return wave_sum(*part_slot(t.chains, r, threadIdx.x & 63u));
 }
 
+// Column of k_gs_full4 workgroup w in cnt's rows (and its inverse).  Workgroups go round-robin to
+// the 8 XCDs, so w and w + 1 run on different L2s; columns grouped per XCD (W is a multiple of 8)
+// let one L2 write whole lines of a row.  Any column order serves: a bucket's segment is filled
+// in column order, and k_gs_tally_count tallies the segment whole.
+#ifndef GP_TALLY_COLXCD
+#define GP_TALLY_COLXCD 1  // A/B knob; 0: column = workgroup index
+#endif
+__device__ __forceinline__ uint32_t tally_col(uint32_t w, uint32_t W) {
+    return GP_TALLY_COLXCD ? (w & 7u) * (W >> 3) + (w >> 3) : w;
+}
+__device__ __forceinline__ uint32_t tally_wg(uint32_t c, uint32_t W) {
+    return GP_TALLY_COLXCD ? (c % (W >> 3)) * 8u + c / (W >> 3) : c;
+}
+
 // The state bytes (st4) and the round r - 1 receipt words of actors v0 .. v0+3.  Deep in a run's
 // tail (deep: block-uniform) a quad of four done actors skips its receipt words: a done actor ignores
 // receipts (program.fs:92), so its words are neither read nor cleared, and whatever lands in them
@@ -1711,7 +1725,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
     }
     if (tally) {  // this workgroup's counts, bucket-major for the scan
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < t.nb; i += kBlock) t.cnt[i * t.W + blockIdx.x] = tcnt[i];
+        for (uint32_t i = threadIdx.x; i < t.nb; i += kBlock) t.cnt[i * t.W + tally_col(blockIdx.x, t.W)] = tcnt[i];
     }
 }
 
@@ -1841,7 +1855,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_tally_scatter(RoundArgs a, GsTall
     if (!t.on[r & 3u]) return;  // uniform
     // this workgroup's first position in every bucket's segment (then LDS atomics give each
     // receipt its place without another global read)
-    for (uint32_t i = threadIdx.x; i < t.nb; i += kBlock) tpos[i] = t.off[i * t.W + blockIdx.x];
+    for (uint32_t i = threadIdx.x; i < t.nb; i += kBlock) tpos[i] = t.off[i * t.W + tally_col(blockIdx.x, t.W)];
     __syncthreads();
     const uint32_t na = a.hi;
     const uint32_t nq = (na + 3u) >> 2;
@@ -1988,7 +2002,7 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
     for (uint32_t k = 0; k < kScatK; ++k) {  // uniform
         // k_gs_full4 workgroup w's walk (node_range, thread lt): its iteration kScatK * i + g is
         // this thread's i-th
-        const uint32_t w = kScatK * sg + k;
+        const uint32_t w = tally_wg(kScatK * sg + k, W);
         const uint32_t base = (w & 7u) * span4;
         const uint32_t end = base >= nq ? 0u : (base + span4 < nq ? base + span4 : nq);
         const uint32_t q0 = base + (w >> 3) * kBlock + lt;
