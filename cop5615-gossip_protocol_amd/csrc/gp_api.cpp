@@ -1483,7 +1483,8 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
                 const size_t nc = (size_t)nb * t.W;
                 if ((rc = h->alloc(&t.cnt, nc)) || (rc = h->alloc(&t.off, nc + 1)) || (rc = h->alloc(&t.tgt, 2 * n)) ||
                     (rc = h->alloc(&t.scratch, scan_scratch_words((uint32_t)nc))) ||
-                    (rc = h->alloc(&t.chains, (size_t)kPartRing * kParts * kPartStride)) || (rc = h->alloc(&t.on, 4)))
+                    (rc = h->alloc(&t.chains, (size_t)kPartRing * kParts * kPartStride)) || (rc = h->alloc(&t.on, 4)) ||
+                    (GP_TALLY_INC16 && (rc = h->alloc(&t.inc16, (n + 7) & ~(size_t)7))))
                     return bail(rc);
             }
         } else if ((rc = h->alloc(&h->dir[0], xn, xlo)) || (rc = h->alloc(&h->dir[1], xn, xlo))) {

@@ -229,6 +229,9 @@ constexpr uint32_t kMaxTallyBuckets = 4096;   // k_gs_full4's LDS counters: 16 K
 #ifndef GP_TALLY_LATE_DIV
 #define GP_TALLY_LATE_DIV 64  // A/B knob; 0: no late tally
 #endif
+#ifndef GP_TALLY_INC16
+#define GP_TALLY_INC16 1  // A/B knob; 0: tallied rounds write the 32-bit receipt words
+#endif
 constexpr uint64_t kTallyLateDiv = GP_TALLY_LATE_DIV;  // also tally (filter on) while >= 1/64 of the nodes are not done
 struct GsTally {
     uint32_t* cnt;     // [nb * W] receipts per (bucket, workgroup), bucket-major; null: no tally
@@ -238,6 +241,8 @@ struct GsTally {
     uint32_t* scratch; // scan scratch (scan_scratch_words(nb * W))
     uint32_t* chains;  // [4][kParts * kPartStride]: chains emitted in round r, ring slot r & 3
     uint32_t* on;      // [4]: round r tallies (written by block 0 of F(r))
+    uint16_t* inc16;   // [actors] receipts of the last tallied round (GP_TALLY_INC16); 0xFFFF: the
+                       // count is in that round's 32-bit receipt word
     uint32_t thr;      // tally in round r >= 1 when round r - 1 emitted at least thr chains to
                        // targets not done yet (estimated from the share of nodes not done)
     uint32_t nb, W;    // buckets; k_gs_full4's grid

@@ -1570,13 +1570,28 @@ __device__ __forceinline__ uint32_t tally_wg(uint32_t c, uint32_t W) {
 #ifndef GP_DEEP_DIV
 #define GP_DEEP_DIV 64  // A/B knob: "deep" = fewer than 1/GP_DEEP_DIV of the nodes not done (0: off)
 #endif
-__device__ __forceinline__ uint4 load_quad(const RoundArgs& a, uint32_t v0, uint32_t r, bool deep, uint32_t& st4) {
+// i16: round r - 1 tallied into 16-bit words (k_gs_tally_count); kInc16Esc sends to the 32-bit word.
+#ifndef GP_INC16_ESC
+#define GP_INC16_ESC 0xFFFF  // test knob: 1 sends every nonzero count through the 32-bit words
+#endif
+constexpr uint32_t kInc16Esc = GP_INC16_ESC;
+// want: the receipt words were due (read).
+__device__ __forceinline__ uint4 load_quad(const RoundArgs& a, const uint16_t* i16, uint32_t v0, uint32_t r, bool deep,
+                                           uint32_t& st4, bool& want) {
     uint4 in4 = make_uint4(0u, 0u, 0u, 0u);
     st4 = *reinterpret_cast<const uint32_t*>(a.gstate + v0);
-    if (deep) {
-        if (r && (st4 & 0x04040404u) != 0x04040404u) in4 = *reinterpret_cast<const uint4*>(a.inc_prev + v0);
-    } else if (r) {
-        in4 = *reinterpret_cast<const uint4*>(a.inc_prev + v0);
+    want = r && (!deep || (st4 & 0x04040404u) != 0x04040404u);
+    if (want) {
+        if (i16) {
+            const uint2 h = *reinterpret_cast<const uint2*>(i16 + v0);
+            in4 = make_uint4(h.x & 0xFFFFu, h.x >> 16, h.y & 0xFFFFu, h.y >> 16);
+            if (in4.x == kInc16Esc) in4.x = a.inc_prev[v0];
+            if (in4.y == kInc16Esc) in4.y = a.inc_prev[v0 + 1u];
+            if (in4.z == kInc16Esc) in4.z = a.inc_prev[v0 + 2u];
+            if (in4.w == kInc16Esc) in4.w = a.inc_prev[v0 + 3u];
+        } else {
+            in4 = *reinterpret_cast<const uint4*>(a.inc_prev + v0);
+        }
     }
     return in4;
 }
@@ -1632,6 +1647,9 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
     // reported; at 10M the bitmap is L2-resident and the filter wins: profiles/round4/c4_late_tally/).
     // Uniform: every block reads the same final counts.
     const bool tally = t.cnt && r >= 1u && t.on[r & 3u];
+    // round r - 1 tallied: its receipts are in t.inc16, and its 32-bit words hold stale counts (the
+    // round before a round that tallies leaves them unzeroed) but for the 0xFFFF escapes
+    const bool from16 = GP_TALLY_INC16 && t.cnt && r >= 2u && t.on[(r - 1u) & 3u];
     const double ch = (t.cnt && r >= 1u) ? (double)tally_chains(t, r - 1u) : 0.0;  // (no tally: no chains array)
     const bool tally_next = t.cnt && r >= 1u && prev < a.target &&
                             (ch * (double)(a.target - prev) >= (double)t.thr * (double)a.target ||
@@ -1665,14 +1683,17 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
         const uint32_t v0 = q << 2;
         uint32_t st4 = 0, done4 = 0;
         if (valid) {
-            uint4 in4 = load_quad(a, v0, r, deep, st4);
+            bool want;
+            uint4 in4 = load_quad(a, from16 ? t.inc16 : nullptr, v0, r, deep, st4, want);
             uint32_t inc[4] = {in4.x, in4.y, in4.z, in4.w};
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
                 if (v0 + j >= na) inc[j] = 0u;  // the padding past the last actor
+            // round r + 1 adds its receipts into the words of round r - 1 unless it tallies: after a
+            // tallied round they are cleared whole (stale), else the consumed ones
+            if (from16 && !tally_next && want) *reinterpret_cast<uint4*>(a.inc_prev + v0) = make_uint4(0u, 0u, 0u, 0u);
             if (inc[0] | inc[1] | inc[2] | inc[3])
-                // consumed; round r + 1 adds its receipts here (a tallied round writes them whole)
-                st4 = gs_apply4(a, v0, st4, inc, !tally_next, done4, newly);
+                st4 = gs_apply4(a, v0, st4, inc, !tally_next && !from16, done4, newly);
             // emit round r: one draw per activation chain (program.fs:89-95)
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j) {
@@ -1761,7 +1782,8 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) mine |= (valid && v0 + j - lo < hi - lo) ? 1u << j : 0u;
         if (mine) {
-            uint4 in4 = load_quad(a, v0, r, deep, st4);
+            bool due;
+            uint4 in4 = load_quad(a, nullptr, v0, r, deep, st4, due);
             uint32_t inc[4] = {in4.x, in4.y, in4.z, in4.w};
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
@@ -2082,7 +2104,8 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
 }
 
 // Tallied round: one workgroup per target bucket counts its receipts in LDS and writes the
-// bucket's whole range of inc_cur (zeros included, so nothing is left to clear).  Its 128 KB of LDS
+// bucket's whole range of t.inc16 (GP_TALLY_INC16; else of inc_cur), zeros included, so nothing is
+// left to clear.  Its 128 KB of LDS
 // admit one workgroup per CU: GP_COUNT_BLOCK threads (A/B knob) keep that many in flight.
 #ifndef GP_COUNT_BLOCK
 #define GP_COUNT_BLOCK 1024
@@ -2101,7 +2124,16 @@ __global__ __launch_bounds__(kCountBlock) void k_gs_tally_count(RoundArgs a, GsT
     __syncthreads();
     const uint32_t base = b << kTallyShift, na = a.hi;
     const uint32_t n = na - base < S ? na - base : S;
-    for (uint32_t i = threadIdx.x; i < n; i += kCountBlock) a.inc_cur[base + i] = h[i];
+    if (GP_TALLY_INC16) {  // 16-bit words (half the bytes here and in F(r + 1)); a count that does
+                           // not fit escapes to the 32-bit word
+        for (uint32_t i = threadIdx.x; i < n; i += kCountBlock) {
+            const uint32_t c = h[i];
+            t.inc16[base + i] = (uint16_t)(c < kInc16Esc ? c : kInc16Esc);
+            if (c >= kInc16Esc) a.inc_cur[base + i] = c;
+        }
+    } else {
+        for (uint32_t i = threadIdx.x; i < n; i += kCountBlock) a.inc_cur[base + i] = h[i];
+    }
 }
 
 // Push-sum on any topology (used for "full"): messages are bucketed by destination with an
