@@ -1631,6 +1631,9 @@ __device__ __forceinline__ uint32_t gs_apply4(const RoundArgs& a, uint32_t v0, u
     return st4;
 }
 
+#ifndef GP_GS_PREFETCH
+#define GP_GS_PREFETCH 0  // A/B knob: 1 loads the next quad before applying this one
+#endif
 __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
     extern __shared__ uint32_t tcnt[];  // tally rounds: receipts per target bucket (t.nb)
     const uint32_t r = a.r;
@@ -1677,6 +1680,15 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
     uint32_t q, end, step;
     node_range(0u, nq, span4, q, end, step);
     uint32_t newly = 0, chains = 0;
+    const uint16_t* i16 = from16 ? t.inc16 : nullptr;
+#if GP_GS_PREFETCH
+    // the next quad's state and receipt words are loaded before this one is applied (only this lane
+    // touches them in this round)
+    uint32_t st_n = 0;
+    bool want_n = false;
+    uint4 in_n = make_uint4(0u, 0u, 0u, 0u);
+    if (q < end) in_n = load_quad(a, i16, q << 2, r, deep, st_n, want_n);
+#endif
     // uniform per wave: the 8 lanes sharing a bitmap word reduce together
     for (; q - (threadIdx.x & 63u) < end; q += step) {
         const bool valid = q < end;
@@ -1684,7 +1696,14 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
         uint32_t st4 = 0, done4 = 0;
         if (valid) {
             bool want;
-            uint4 in4 = load_quad(a, from16 ? t.inc16 : nullptr, v0, r, deep, st4, want);
+#if GP_GS_PREFETCH
+            uint4 in4 = in_n;
+            st4 = st_n;
+            want = want_n;
+            if (q + step < end) in_n = load_quad(a, i16, (q + step) << 2, r, deep, st_n, want_n);
+#else
+            uint4 in4 = load_quad(a, i16, v0, r, deep, st4, want);
+#endif
             uint32_t inc[4] = {in4.x, in4.y, in4.z, in4.w};
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
