@@ -100,7 +100,10 @@ int sizes(int64_t n_arg, int32_t topology, int64_t* nodes, int64_t* actors, int6
 // Layout of one exchange chunk (peer p -> peer q); both ends compute it identically.
 struct Chunk {
     size_t hdir = 0, hslot = 0, hmsg = 0, slot = 0, msg = 0, size = 0;  // byte offsets / total size
-    size_t done = 0;    // full gossip: the sender's done-bitmap words (0: none)
+    size_t tail = 0;    // first byte after the header and the halo face (the parts a plan resizes)
+    size_t done = 0;    // full gossip: the sender's done part (0: none)
+    uint32_t dwords = 0;  // full gossip: done-bitmap words of the sender's range
+    uint32_t dpairs = 0;  // done part as (index, word) pairs (capacity); 0: every word
     uint32_t halo = 0;  // halo actors carried (0: none)
     uint32_t hcap = 0;  // halo entries: push-sum messages crossing the face
     uint32_t cap = 0;   // link / receipt entries
@@ -132,6 +135,9 @@ struct Ckpt {
     uint32_t* inc = nullptr;
     uint32_t* dbits = nullptr;
     uint32_t* dsum = nullptr;
+    uint32_t* dship = nullptr;  // the own words as shipped (lazy done-word shipping)
+    int64_t gj = 0;             // the per-round plan's chain count at that round
+    double gcj = 1.0;
     bool allocated = false;
 };
 
@@ -154,6 +160,24 @@ struct Handle {
     uint32_t max_in_cap = 0;
     std::vector<Chunk> full_out, full_in;  // the full plan (the buffers are sized for it)
     uint32_t* pmax = nullptr;      // running max of link entries per sub-segment to each peer
+    // full gossip shards: a plan per round.  Inputs every rank holds alike: the global
+    // chain count cj emitted in round j (chains at most double per round), and per chunk the last
+    // round's largest sub-segment count (m_out from this rank's pack, m_in from the peer's header) and
+    // dirty done words (dw_out / dw_in).
+    uint32_t* cparts = nullptr;               // chains emitted per round: kPartRing x kParts sub-counters
+    unsigned long long* self_chains = nullptr;
+    uint32_t* pstat = nullptr;                // kPstatWords: the last round's plan inputs (kPs*)
+    uint32_t* dship = nullptr;                // own done words as last shipped
+    uint32_t* dstat = nullptr;                // kDstatWords: dirty-word counter, backlog flag
+    struct GossipPlan {
+        bool on = false;    // sized plans (else the full plan); a restore point exists
+        bool seen = false;  // m / dw hold a round's counts
+        int64_t j = 0;      // round whose global chain count is cj
+        double cj = 1.0;
+        std::vector<uint32_t> m_out, m_in, dw_in;
+        uint32_t dw_out = 0;
+    } gpl;
+    int64_t bytes_sent = 0;        // exchange bytes this rank sent since the last reset (replays included)
     const void* last_recv = nullptr;  // the receive buffer of the last gp_shard_deliver
     Ckpt ck;                       // activity tiers: the restore point (push-sum shards)
     int64_t full_until = 0;        // after a restore: the full plan until this many rounds are final
@@ -283,6 +307,7 @@ struct Handle {
         a.term_limit = (uint32_t)cfg.term_limit;
         a.total = total;
         a.parts = parts;
+        a.cparts = cparts;
         a.rev_off = rev_off;
         a.rev_src = rev_src;
         a.lpos = lpos;
@@ -471,8 +496,15 @@ int clear_act(Handle* h, int i) {
 // Full gossip's done bitmap over every actor (one bit each) and its summary (one bit per word).
 size_t dbits_words_all(const Handle* h) { return ((size_t)h->g.actors + 31u) / 32u + 1u; }
 size_t dsum_words_all(const Handle* h) { return ((size_t)h->g.actors + 1023u) / 1024u + 1u; }
+// a shard's own words of it (global word index (lo >> 5) on)
+size_t dship_words(const Handle* h) { return (size_t)(((h->hi - 1u) >> 5) - (h->lo >> 5) + 1u); }
 
 void full_plan(Handle* h);
+bool tiers_on(const Handle* h);
+bool gossip_plans(const Handle* h);
+void gossip_round_plan(Handle* h, int64_t k);
+int ensure_ckpt(Handle* h);
+int ckpt_copy(Handle* h, bool save);
 
 int reset(Handle* h) {
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -546,13 +578,34 @@ int reset(Handle* h) {
     h->timed_count = 0;
     if (h->sharded) {  // the full plan, no restore point
         HIP_TRY(hipMemsetAsync(h->pmax, 0, kMaxWorld * sizeof(uint32_t), h->stream));
+        if (h->cparts) {  // full gossip's per-round plan inputs and done-word shipping state
+            HIP_TRY(hipMemsetAsync(h->cparts, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t), h->stream));
+            HIP_TRY(hipMemsetAsync(h->pstat, 0, kPstatWords * sizeof(uint32_t), h->stream));
+            HIP_TRY(hipMemsetAsync(h->dstat, 0, kDstatWords * sizeof(uint32_t), h->stream));
+            HIP_TRY(hipMemsetAsync(h->dship + (h->lo >> 5), 0, dship_words(h) * sizeof(uint32_t), h->stream));
+        }
         HIP_TRY(hipStreamSynchronize(h->stream));
         h->ck.valid = false;
         h->tiered = false;
         h->delivered = 0;
         h->full_until = 0;
         h->last_recv = nullptr;
+        h->bytes_sent = 0;
         if (!h->full_out.empty()) full_plan(h);
+        if (gossip_plans(h) && !h->full_out.empty()) {
+            // round 0's chains: the leader's one (program.fs:218); the sized plans run from round 0, so
+            // the restore point is the initial state
+            Handle::GossipPlan& P = h->gpl;
+            P = Handle::GossipPlan{};
+            P.m_out.assign((size_t)h->world, 0u);
+            P.m_in.assign((size_t)h->world, 0u);
+            P.dw_in.assign((size_t)h->world, 0u);
+            P.on = tiers_on(h);
+            int rc;
+            if (P.on && ((rc = ensure_ckpt(h)) || (rc = ckpt_copy(h, true)))) return rc;
+            h->tiered = P.on;
+            gossip_round_plan(h, 0);
+        }
     }
     return GP_OK;
 }
@@ -694,8 +747,8 @@ constexpr int64_t kTimeGroup = GP_TIME_GROUP;
 #ifndef GP_TAIL_BATCH
 #define GP_TAIL_BATCH 32
 #endif
-constexpr int64_t kTailBatch = GP_TAIL_BATCH;
-constexpr int64_t kMaxBatch = 256;  // rounds per gp_step batch at most  // rounds per batch in a run's tail (0: no tail rule)
+constexpr int64_t kTailBatch = GP_TAIL_BATCH;  // rounds per batch in a run's tail (0: no tail rule)
+constexpr int64_t kMaxBatch = 256;             // rounds per gp_step batch at most
 
 int ensure_events(Handle* h, int64_t rounds) {
     const size_t need = (size_t)(3 * rounds);
@@ -887,6 +940,37 @@ uint32_t entry_cap_sub(double mean, double exact_max) {
     return (uint32_t)std::max(1.0, std::min(c, exact_max));
 }
 
+// Actors of rank p whose chains share one sub-segment of its chunks (k_gs_full4x: the sub-segment of
+// a block-iteration is its 1024-actor chunk index mod kSub, so one holds ceil(chunks / kSub) chunks).
+int64_t gs_sub_actors(const Handle* h, int p) {
+    const int64_t size_p = h->abnd[p + 1] - h->abnd[p];
+    const int64_t q0 = (h->abnd[p] >> 2) & ~7LL, q1 = (h->abnd[p + 1] + 3) >> 2;
+    const int64_t chunks = ((q1 - 1) >> 8) - (q0 >> 8) + 1, per_sub = (chunks + kSub - 1) / kSub;
+    return std::min<int64_t>(size_p, per_sub * 1024);
+}
+
+// The chunk `full` with `cap` entries per sub-segment and a done part of `dpairs` pairs (0: every
+// word); the header and the halo face are unchanged.
+Chunk shaped(const Chunk& full, uint32_t cap, uint32_t dpairs) {
+    Chunk c = full;
+    c.cap = cap;
+    c.dpairs = full.done ? dpairs : 0u;
+    size_t off = c.tail;
+    if (full.done) {
+        c.done = off;
+        off = align_up(off + (c.dpairs ? (size_t)c.dpairs * 2 * sizeof(uint32_t) : (size_t)c.dwords * sizeof(uint32_t)));
+    }
+    c.slot = off;
+    off = align_up(off + (size_t)kSub * cap * sizeof(uint32_t));
+    c.msg = 0;
+    if (full.msg) {
+        c.msg = off;
+        off = align_up(off + (size_t)kSub * cap * sizeof(double2));
+    }
+    c.size = off;
+    return c;
+}
+
 Chunk chunk_layout(const Handle* h, int p, int q) {
     Chunk c;
     size_t off = kAlign;  // ShardHeader
@@ -910,19 +994,19 @@ Chunk chunk_layout(const Handle* h, int p, int q) {
             off = align_up(off + (size_t)kSub * c.hcap * sizeof(double2));
         }
     }
+    c.tail = off;
     if (h->full && h->gossip) {  // the sender's done-bitmap words, words (lo_p >> 5) .. ((hi_p - 1) >> 5)
         c.done = off;
-        off = align_up(off + (size_t)(((h->abnd[p + 1] - 1) >> 5) - (h->abnd[p] >> 5) + 1) * sizeof(uint32_t));
+        c.dwords = (uint32_t)(((h->abnd[p + 1] - 1) >> 5) - (h->abnd[p] >> 5) + 1);
     }
     double mean = 0.0, exact = 0.0;
     if (h->full) {
-        // every chain of p draws a target uniform over the other actors.  k_gs_full4x picks a
-        // sub-segment per 1024-actor chunk of p's range (chunk index mod kSub), so a sub-segment sees
-        // the chains of ceil(chunks / kSub) chunks at most: entry_cap_sub gets kSub times that
-        const int64_t q0 = (h->abnd[p] >> 2) & ~7LL, q1 = (h->abnd[p + 1] + 3) >> 2;
-        const int64_t chunks = ((q1 - 1) >> 8) - (q0 >> 8) + 1, per_sub = (chunks + kSub - 1) / kSub;
+        // every chain of p draws a target uniform over the other actors, and on "full" an actor holds
+        // one chain at most (the leader's kick-off is its first receipt, program.fs:218, so no actor
+        // gains a second one, :99-100).  A sub-segment sees the chains of gs_sub_actors actors:
+        // entry_cap_sub gets kSub times that
         const double share = (double)(h->abnd[q + 1] - h->abnd[q]) / (double)h->lay.nodes;
-        const double chains = 2.0 * (double)std::min<int64_t>(size_p, per_sub * 1024);
+        const double chains = (double)gs_sub_actors(h, p);
         mean = (double)kSub * chains * share;
         exact = chains;  // one sub-segment's bound
     } else if (h->g.has_link) {
@@ -935,39 +1019,22 @@ Chunk chunk_layout(const Handle* h, int p, int q) {
     }
     c.cap = entry_cap_sub(mean, exact);
     if (exact == 0.0) c.cap = 0;
-    c.slot = off;
-    off = align_up(off + (size_t)kSub * c.cap * sizeof(uint32_t));
-    if (!h->gossip) {
-        c.msg = off;
-        off = align_up(off + (size_t)kSub * c.cap * sizeof(double2));
-    }
-    c.size = off;
-    return c;
-}
-
-// The chunk `full` with `cap` link entries per sub-segment (the header and halo part unchanged).
-Chunk with_cap(const Chunk& full, uint32_t cap) {
-    Chunk c = full;
-    c.cap = cap;
-    size_t off = align_up(c.slot + (size_t)kSub * cap * sizeof(uint32_t));
-    if (full.msg) {
-        c.msg = off;
-        off = align_up(off + (size_t)kSub * cap * sizeof(double2));
-    }
-    c.size = off;
-    return c;
+    if (!h->gossip) c.msg = 1;  // (shaped() places the messages)
+    return shaped(c, c.cap, 0);
 }
 
 // The current plan: chunk p -> q of every peer with the link capacities out_cap[q] / in_cap[q]
-// (the full plan's at most), packed from offset 0 of the send / receive buffers.
-void apply_plan(Handle* h, const std::vector<uint32_t>& out_cap, const std::vector<uint32_t>& in_cap) {
+// (the full plan's at most) and done parts of out_dp[q] / in_dp[q] pairs (0: every word), packed
+// from offset 0 of the send / receive buffers.
+void apply_plan(Handle* h, const std::vector<uint32_t>& out_cap, const std::vector<uint32_t>& in_cap,
+                const std::vector<uint32_t>* out_dp = nullptr, const std::vector<uint32_t>* in_dp = nullptr) {
     const int W = h->world;
     int64_t so = 0, ro = 0;
     h->max_in_cap = 0;
     for (int q = 0; q < W; ++q) {
         if (q != h->rank) {
-            h->out_chunk[q] = with_cap(h->full_out[q], std::min(out_cap[q], h->full_out[q].cap));
-            h->in_chunk[q] = with_cap(h->full_in[q], std::min(in_cap[q], h->full_in[q].cap));
+            h->out_chunk[q] = shaped(h->full_out[q], std::min(out_cap[q], h->full_out[q].cap), out_dp ? (*out_dp)[q] : 0u);
+            h->in_chunk[q] = shaped(h->full_in[q], std::min(in_cap[q], h->full_in[q].cap), in_dp ? (*in_dp)[q] : 0u);
             h->max_in_cap = std::max(h->max_in_cap, h->in_chunk[q].cap);
         }
         h->out_off[q] = so;
@@ -1027,6 +1094,10 @@ Xchg base_xchg(const Handle* h) {
     x.self_newly = h->self_newly;
     x.pmax = h->pmax;
     x.slot_dst = h->slot_dst;
+    x.self_chains = h->self_chains;
+    x.pstat = h->pstat;
+    x.dship = h->dship;
+    x.dstat = h->dstat;
     return x;
 }
 
@@ -1038,14 +1109,14 @@ Xchg make_xchg(const Handle* h, void* send, const void* recv) {
             char* b = static_cast<char*>(send) + h->out_off[q];
             const Chunk& c = h->out_chunk[q];
             x.out[q] = PeerOut{reinterpret_cast<ShardHeader*>(b), reinterpret_cast<uint32_t*>(b + c.slot),
-                               c.msg ? reinterpret_cast<double2*>(b + c.msg) : nullptr, c.cap,
+                               c.msg ? reinterpret_cast<double2*>(b + c.msg) : nullptr, c.cap, c.dpairs,
                                c.done ? reinterpret_cast<uint32_t*>(b + c.done) : nullptr};
         }
         if (recv) {
             const char* b = static_cast<const char*>(recv) + h->in_off[q];
             const Chunk& c = h->in_chunk[q];
             x.in[q] = PeerIn{reinterpret_cast<const ShardHeader*>(b), reinterpret_cast<const uint32_t*>(b + c.slot),
-                             c.msg ? reinterpret_cast<const double2*>(b + c.msg) : nullptr, c.cap,
+                             c.msg ? reinterpret_cast<const double2*>(b + c.msg) : nullptr, c.cap, c.dpairs,
                              c.done ? reinterpret_cast<const uint32_t*>(b + c.done) : nullptr};
         }
     }
@@ -1113,6 +1184,7 @@ int shard_round(Handle* h, void* send) {
     HIP_TRY(hipGetLastError());
     h->awaiting_deliver = true;
     h->pending_send = send;
+    for (int q = 0; q < h->world; ++q) h->bytes_sent += (int64_t)h->out_chunk[q].size;
     return GP_OK;
 }
 
@@ -1136,6 +1208,7 @@ int shard_deliver(Handle* h, const void* recv) {
     h->last_recv = recv;
     ++h->delivered;
     h->next_kernel = k + 1;
+    if (gossip_plans(h)) gossip_round_plan(h, h->next_kernel);  // full gossip: a plan per round
     return GP_OK;
 }
 
@@ -1169,6 +1242,67 @@ uint32_t tier_cap(uint32_t full, uint32_t m, bool tight) {
     return c;
 }
 
+// ---- full gossip shards: a plan per round
+// A full-gossip run ramps up (chains double per round for ~log2(actors) rounds, nearly nothing moves),
+// saturates (every actor sends), then thins out as targets report and the senders filter them; a
+// batch-wide plan ships the saturated capacity through the ramp.  Here each round k gets its own
+// plan, computed alike at both ends of a chunk from values both hold:
+//   * entries: round k's chains are at most cj * 2^(k - j) (a new chain needs a receipt, and a receipt
+//     a chain), the chain holders are uniform over the actors, so a sub-segment of p -> q holds at most
+//     mean + 8 sigma + 64 of that bound's share (the full plan's own rule), and, once a round was
+//     seen, at most twice its largest sub-segment scaled by the same growth, plus 64;
+//   * done words: the dirty words of the last round, doubled, plus 64, as (index, word) pairs, or
+//     every word once pairs would cost as much.  Words past the capacity wait (k_shard_done_out).
+// Counts can outgrow a sized chunk (statistics, not bounds): overflow is detected, and the batch
+// replays from the restore point with the full plan, as under the push-sum tiers.
+bool gossip_plans(const Handle* h) { return h->sharded && h->world > 1 && h->gossip && h->full; }
+
+uint32_t gs_cap(const Handle* h, int p, int q, int64_t k, uint32_t m, uint32_t full_cap) {
+    const Handle::GossipPlan& P = h->gpl;
+    if (!P.on) return full_cap;
+    const bool tight = (h->cfg.flags & GP_FLAG_TIGHT_TIERS) != 0;
+    const double A = (double)h->g.actors;
+    const int64_t dk = std::max<int64_t>(k - P.j, 0);
+    const double cb = dk >= 62 ? A : std::min(A, P.cj * std::ldexp(1.0, (int)dk));
+    const double n_sub = (double)gs_sub_actors(h, p);
+    const double share = (double)(h->abnd[q + 1] - h->abnd[q]) / (double)h->lay.nodes;
+    const double mean = cb * n_sub / A * share;
+    double c = tight ? std::ceil(mean) : (double)entry_cap_sub((double)kSub * mean, std::min(cb, n_sub));
+    if (P.seen) {
+        const double grow = P.cj > 0.0 ? cb / P.cj : 1.0;
+        c = std::min(c, tight ? std::ceil((double)m * grow) : std::ceil(2.0 * (double)m * grow + 64.0));
+    }
+    return (uint32_t)std::min(c, (double)full_cap);
+}
+
+uint32_t gs_dpairs(const Handle* h, int p, uint32_t dw) {
+    if (!h->gpl.on) return 0u;
+    const bool tight = (h->cfg.flags & GP_FLAG_TIGHT_TIERS) != 0;
+    // the report wave (from 1/1024 of the nodes reported until 1/64 are left): nearly every word
+    // changes every round, and a stale replica weakens the sender filter just as it turns on (1/16):
+    // every word, so the replicas stay a round behind at most
+    const int64_t n = h->lay.nodes, c = h->completed;
+    if (!tight && c * 1024 >= n && (n - c) * 64 >= n) return 0u;
+    const uint64_t nw = (uint64_t)(((h->abnd[p + 1] - 1) >> 5) - (h->abnd[p] >> 5) + 1);
+    const uint64_t d = tight ? dw / 2u + 1u : 2ull * dw + 64u;  // tight: a backlog in most rounds
+    return 2u * d >= nw ? 0u : (uint32_t)d;
+}
+
+// Round k's plan (k = the next round gp_shard_round packs).
+void gossip_round_plan(Handle* h, int64_t k) {
+    const int W = h->world, p = h->rank;
+    const Handle::GossipPlan& P = h->gpl;
+    std::vector<uint32_t> oc((size_t)W, 0u), ic((size_t)W, 0u), od((size_t)W, 0u), id((size_t)W, 0u);
+    for (int q = 0; q < W; ++q) {
+        if (q == p) continue;
+        oc[q] = gs_cap(h, p, q, k, P.seen ? P.m_out[q] : 0u, h->full_out[q].cap);
+        ic[q] = gs_cap(h, q, p, k, P.seen ? P.m_in[q] : 0u, h->full_in[q].cap);
+        od[q] = gs_dpairs(h, p, P.seen ? P.dw_out : 0u);
+        id[q] = gs_dpairs(h, q, P.seen ? P.dw_in[q] : 0u);
+    }
+    apply_plan(h, oc, ic, &od, &id);
+}
+
 int ensure_ckpt(Handle* h) {
     Ckpt& c = h->ck;
     if (c.allocated) return GP_OK;
@@ -1176,7 +1310,7 @@ int ensure_ckpt(Handle* h) {
     int rc;
     if (h->gossip) {  // full gossip
         if ((rc = h->alloc(&c.cnt, n)) || (rc = h->alloc(&c.gstate, n)) || (rc = h->alloc(&c.inc, n)) ||
-            (rc = h->alloc(&c.dbits, dbits_words_all(h))))
+            (rc = h->alloc(&c.dbits, dbits_words_all(h))) || (h->dship && (rc = h->alloc(&c.dship, dship_words(h)))))
             return rc;
         if (h->dsum && (rc = h->alloc(&c.dsum, dsum_words_all(h)))) return rc;
         c.allocated = true;
@@ -1208,8 +1342,20 @@ int ckpt_copy(Handle* h, bool save) {
         HIP_TRY(cp(h->inc[p] + lo, c.inc, n * sizeof(uint32_t)));
         HIP_TRY(cp(h->dbits, c.dbits, dbits_words_all(h) * sizeof(uint32_t)));
         if (h->dsum) HIP_TRY(cp(h->dsum, c.dsum, dsum_words_all(h) * sizeof(uint32_t)));
+        if (h->dship) HIP_TRY(cp(h->dship + (lo >> 5), c.dship, dship_words(h) * sizeof(uint32_t)));
         // round k0's receipts accumulate in the other array, empty before F(k0): a failed batch's go
         if (!save) HIP_TRY(hipMemsetAsync(h->inc[p ^ 1] + lo, 0, n * sizeof(uint32_t), s));
+        if (save) {
+            c.gj = h->gpl.j;
+            c.gcj = h->gpl.cj;
+        } else if (h->dstat) {
+            // the shipping state of the restore point: no round counted, and a scan in the next round
+            // (whatever was left dirty then is found again)
+            HIP_TRY(hipMemsetAsync(h->dstat, 0, kDstatWords * sizeof(uint32_t), s));
+            const uint32_t one = 1u;
+            HIP_TRY(hipMemcpyAsync(h->dstat + kDstatLeft, &one, sizeof one, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipStreamSynchronize(s));
+        }
     } else {
     HIP_TRY(cp(h->msg[p] + xlo, c.msg, xn * sizeof(double2)));
     HIP_TRY(cp(h->dir[p] + xlo, c.dir, xn));
@@ -1246,10 +1392,17 @@ int restore(Handle* h, int64_t reached) {
     if ((rc = ckpt_copy(h, false))) return rc;
     hipStream_t s = h->stream;
     HIP_TRY(hipMemsetAsync(h->parts, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t), s));
+    if (h->cparts) HIP_TRY(hipMemsetAsync(h->cparts, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(h->pcount, 0, ((size_t)h->world + 2) * kSub * kCtrStride * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(h->overflow, 0, sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(h->pmax, 0, kMaxWorld * sizeof(uint32_t), s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (gossip_plans(h)) {  // the chain count of the restore point; no round seen since
+        h->gpl.j = c.gj;
+        h->gpl.cj = c.gcj;
+        h->gpl.seen = false;
+        h->gpl.on = false;
+    }
     h->rounds = c.rounds;
     h->completed = c.completed;
     h->converged = false;
@@ -1304,6 +1457,38 @@ int choose_plan(Handle* h) {
     return GP_OK;
 }
 
+// Full gossip: the inputs of the next rounds' plans (the last round's counts), a restore point when
+// one is due, and the plan of the next round.
+int gossip_sync(Handle* h) {
+    Handle::GossipPlan& P = h->gpl;
+    const bool tight = (h->cfg.flags & GP_FLAG_TIGHT_TIERS) != 0;
+    if (h->delivered && h->last_recv) {
+        h->delivered = 0;
+        uint32_t ps[kPstatWords];
+        HIP_TRY(hipMemcpy(ps, h->pstat, sizeof ps, hipMemcpyDeviceToHost));
+        unsigned long long c;
+        std::memcpy(&c, ps + kPsChains, sizeof c);
+        P.j = h->next_kernel - 1;  // the chains F(next_kernel - 1) emitted
+        P.cj = (double)c;
+        P.dw_out = ps[kPsDirty];
+        for (int q = 0; q < h->world; ++q) {
+            P.m_out[q] = ps[kPsOut + q];
+            P.m_in[q] = ps[kPsIn + q];
+            P.dw_in[q] = ps[kPsDwIn + q];
+        }
+        P.seen = true;
+    }
+    P.on = tiers_on(h) && !h->converged && h->rounds >= h->full_until;
+    if (P.on && (!h->ck.valid || tight || h->rounds - h->ck.rounds >= kCkptEvery)) {
+        int rc;
+        if ((rc = ensure_ckpt(h)) || (rc = ckpt_copy(h, true))) return rc;
+    }
+    h->tiered = P.on;
+    gossip_round_plan(h, h->next_kernel);
+    ++h->plan_changes;
+    return GP_OK;
+}
+
 int shard_sync(Handle* h, gp_status* st) {
     if (h->awaiting_deliver) return fail(GP_ESTATE, "gp_shard_sync between gp_shard_round and gp_shard_deliver");
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1347,7 +1532,11 @@ int shard_sync(Handle* h, gp_status* st) {
     if (h->timed_count && (rc = accumulate_timing(h, timed_real))) return rc;
     if (h->timed_count) h->work_rounds += timed_real;  // the quiet kernel counts in timed rounds only
     h->timed_count = 0;
-    if (tiers_on(h) && (rc = choose_plan(h))) return rc;
+    if (gossip_plans(h)) {
+        if ((rc = gossip_sync(h))) return rc;
+    } else if (tiers_on(h) && (rc = choose_plan(h))) {
+        return rc;
+    }
     if (st) {
         std::memset(st, 0, sizeof *st);
         st->round = h->rounds;
@@ -1471,6 +1660,13 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
                 if ((rc = h->alloc(&h->dbits, dbits_words_all(h)))) return bail(rc);
                 if (A >= kDsumMinActors && (rc = h->alloc(&h->dsum, dsum_words_all(h)))) return bail(rc);
             }
+            // full gossip on shards: the per-round plans' inputs and the lazy done-word shipping
+            if (h->sharded && h->world > 1 && h->full &&
+                ((rc = h->alloc(&h->cparts, (size_t)kPartRing * kParts * kPartStride)) ||
+                 (rc = h->alloc(&h->self_chains, 1)) || (rc = h->alloc(&h->pstat, kPstatWords)) ||
+                 (rc = h->alloc(&h->dstat, kDstatWords)) ||
+                 (rc = h->alloc(&h->dship, dship_words(h), (int64_t)(h->lo >> 5)))))
+                return bail(rc);
             const uint32_t nb = (uint32_t)((n + (1u << kTallyShift) - 1) >> kTallyShift);
             // the tally is a speed path: where its 128 KB of dynamic LDS cannot be allowed (another
             // ARCH), the handle keeps the receipt atomics, which give the same results
@@ -1520,6 +1716,9 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
     }
     if (g.has_link && (rc = build_links(h))) return bail(rc);
     if (h->sharded && (rc = build_plan(h))) return bail(rc);
+    // the restore point of the activity tiers, allocated here so that device_bytes counts it and a
+    // shard that fits at creation cannot fail for memory in the middle of a run
+    if (tiers_on(h) && (rc = ensure_ckpt(h))) return bail(rc);
     if ((rc = h->alloc(&h->parts, (size_t)kPartRing * kParts * kPartStride))) return bail(rc);
     // Set up here what gp_step would otherwise allocate inside the timed round loop of a first run
     // (pinned host memory and device reallocations cost 0.1-1 ms each: `1000 full gossip` ran in
@@ -1710,6 +1909,7 @@ int group_step(Handle* h, int64_t max_rounds, gp_status* st) {
     int rc;
     // gossip's F(k) reports round k-1: a batch may run past the convergence round; those
     // rounds are no-ops on the device (gated) and the counts stay final
+    if (gossip_plans(G.shard[0])) G.batch = std::min<int64_t>(G.batch, 4);
     while (!G.converged && G.rounds < goal) {
         const int64_t B = std::min<int64_t>(G.batch, goal - G.rounds);
         for (int64_t i = 0; i < B; ++i) {
@@ -1727,8 +1927,11 @@ int group_step(Handle* h, int64_t max_rounds, gp_status* st) {
         if ((rc = group_sync(G, sts))) return rc;
         // batches start again from 8 rounds when the run enters the half-reported phase, where the
         // activity tiers begin (a plan is chosen at every sync; sharded.py _next_batch does the same)
+        // (full gossip sizes every round from the last round before a sync: 4 rounds at most, §6.10)
         const int64_t nodes = G.shard[0]->lay.nodes;
-        G.batch = (2 * before < nodes && nodes <= 2 * G.completed) ? 8 : std::min<int64_t>(G.batch * 2, 64);
+        const int64_t most = gossip_plans(G.shard[0]) ? 4 : 64;
+        G.batch = (2 * before < nodes && nodes <= 2 * G.completed) ? std::min<int64_t>(8, most)
+                                                                  : std::min<int64_t>(G.batch * 2, most);
     }
     if (sts.empty() && (rc = group_sync(G, sts))) return rc;
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -2129,6 +2332,7 @@ int gp_shard_stats(void* handle, gp_shard_counters* out) {
         out->recv_bytes += (int64_t)h->in_chunk[q].size;
     }
     out->restore_round = h->ck.valid ? h->ck.rounds : -1;
+    out->bytes_sent = h->bytes_sent;
     return GP_OK;
 }
 

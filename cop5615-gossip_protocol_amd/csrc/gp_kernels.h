@@ -26,6 +26,16 @@ constexpr int kMaxWorld = 16;
 // 8 loopback shards: one counter per peer cost 8.5 ms per round).
 constexpr uint32_t kSub = 16;
 constexpr uint32_t kCtrStride = 32;  // u32 words between counters
+// Full gossip's done-word shipping state (Xchg::dstat), one 128 B line each: the dirty-word counter of
+// the round (k_shard_done_out adds, the pack reads and zeroes), the backlog flag (words left dirty
+// after a capped round) and the last round's dirty count (read by the host at a sync).
+constexpr uint32_t kDstatCount = 0, kDstatLeft = 32, kDstatWords = 64;
+// The per-round plan's inputs the host reads at a sync, in one 256-byte array (Xchg::pstat, u32 words):
+// every rank's chains of the last round delivered (u64), this rank's dirty done words of that round,
+// and per peer its largest sub-segment sent (pack), received (unpack, from the header) and the peer's
+// dirty words (unpack).
+constexpr uint32_t kPsChains = 0, kPsDirty = 2, kPsOut = 16, kPsIn = 32, kPsDwIn = 48, kPstatWords = 64;
+static_assert(kPsOut + kMaxWorld <= kPsIn && kPsDwIn + kMaxWorld <= kPstatWords, "pstat layout");
 
 // Single-GPU Imp3D push-sum: the round kernel writes the link marks of its own messages (no
 // k_link_count pass; 1% faster than the separate pass at 10M).  GP_FUSE_LINK=0: the pass.
@@ -68,6 +78,8 @@ struct RoundArgs {
     uint32_t ps_tags;      // push-sum: link marks are round tags (link_tag); gossip: chain counts
     unsigned long long* total;  // total[a] = completion count after round a (trace)
     uint32_t* parts;            // kPartRing x kParts padded sub-counters of newly reported actors
+    uint32_t* cparts;           // full gossip shards: the same ring for the chains emitted in round r
+                                // (F(r) adds, the pack of round r reads; null: not counted)
     // topology side data (Imp3D)
     const uint32_t* rev_off;  // CSR of link sources per destination, ascending
     const uint32_t* rev_src;
@@ -135,6 +147,12 @@ struct ShardHeader {
                                // ends size the next batch's chunk from it
     uint32_t nlinks[kSub];     // link entries written per sub-segment (<= cap)
     uint32_t nhalo[kSub];      // halo entries written per sub-segment (<= hcap)
+    // full gossip
+    uint32_t chains;           // activation chains the sender's actors emitted in the round
+    uint32_t ndone;            // done part: (index, word) pairs written, or (whole-word plan) 1 when
+                               // the words were written, 0 when no word changed
+    uint32_t dwant;            // the sender's own done words that differed from what it had shipped
+                               // (before the pair capacity): both ends size the next done parts from it
 };
 static_assert(sizeof(ShardHeader) <= 256, "the chunk header is 256 bytes");
 
@@ -143,7 +161,8 @@ struct PeerOut {
     uint32_t* slot;
     double2* msg;
     uint32_t cap;
-    uint32_t* done;  // full gossip: the sender's done-bitmap words (its range), or null
+    uint32_t dpairs;  // full gossip: the done part holds up to dpairs (index, word) pairs; 0: every word
+    uint32_t* done;   // full gossip: the sender's done-bitmap words (its range) or pairs, or null
 };
 
 struct PeerIn {
@@ -151,6 +170,7 @@ struct PeerIn {
     const uint32_t* slot;
     const double2* msg;
     uint32_t cap;
+    uint32_t dpairs;
     const uint32_t* done;
 };
 
@@ -181,6 +201,11 @@ struct Xchg {
                                    // peer (reset when the host chooses the plan)
     const uint32_t* slot_dst;      // push-sum, quiet tail: the receiver of each own link slot (the
                                    // unpack marks the segment of a remote link message's receiver)
+    // full gossip: the per-round plan's inputs
+    unsigned long long* self_chains;  // this rank's chains of the round (pack -> unpack)
+    uint32_t* pstat;                  // [kPstatWords] the plan inputs of the last round (-> host; kPs*)
+    uint32_t* dship;                  // own done words as last shipped (global word index)
+    uint32_t* dstat;                  // [kDstatWords]: dirty-word counter, backlog flag
     PeerOut out[kMaxWorld];
     PeerIn in[kMaxWorld];
     HaloX h;

@@ -1232,21 +1232,33 @@ __global__ __launch_bounds__(kBlock) void k_shard_halo(RoundArgs a, Xchg x, int 
 static_assert(kMaxWorld * kSub == kBlock, "k_shard_pack maps one thread per (peer, sub-segment)");
 
 __global__ __launch_bounds__(kBlock) void k_shard_pack(RoundArgs a, Xchg x, long long applied) {
-    __shared__ unsigned long long newly_s;
-    __shared__ uint32_t of_s[kMaxWorld], max_s[kMaxWorld];
+    __shared__ unsigned long long newly_s, chains_s;
+    __shared__ uint32_t of_s[kMaxWorld], max_s[kMaxWorld], last_s[kMaxWorld], dirty_s;
     if (threadIdx.x < 64) {
-        unsigned long long newly = 0;
+        unsigned long long newly = 0, chains = 0;
         if (applied >= 0) newly = *part_slot(a.parts, applied, threadIdx.x);
+        if (a.cparts) chains = *part_slot(a.cparts, a.r, threadIdx.x);
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) newly += __shfl_xor(newly, off, 64);
+        for (int off = 32; off > 0; off >>= 1) {
+            newly += __shfl_xor(newly, off, 64);
+            chains += __shfl_xor(chains, off, 64);
+        }
         if (threadIdx.x == 0) {
             *x.self_newly = newly;
             newly_s = newly;
+            chains_s = chains;
+            if (x.self_chains) *x.self_chains = chains;
+            dirty_s = 0u;
+            if (x.dstat) {  // full gossip: the round's dirty done words (k_shard_done_out); the counter restarts
+                dirty_s = x.dstat[kDstatCount];
+                x.dstat[kDstatCount] = 0u;
+            }
         }
     }
     if (threadIdx.x < kMaxWorld) {
         of_s[threadIdx.x] = 0u;
         max_s[threadIdx.x] = 0u;
+        last_s[threadIdx.x] = 0u;
     }
     __syncthreads();
     const uint32_t q = threadIdx.x / kSub, s = threadIdx.x % kSub;
@@ -1257,6 +1269,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(RoundArgs a, Xchg x, long
         const uint32_t c = *lc;
         hd->nlinks[s] = c < x.out[q].cap ? c : x.out[q].cap;
         atomicMax(&max_s[q], c);
+        atomicMax(&last_s[q], hd->nlinks[s]);
         bool of = c > x.out[q].cap;
         *lc = 0u;
         const int side = q + 1 == x.rank ? 0 : q == x.rank + 1 ? 1 : -1;
@@ -1278,6 +1291,20 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(RoundArgs a, Xchg x, long
         const uint32_t m = max_s[q] > x.pmax[q] ? max_s[q] : x.pmax[q];  // one writer per peer
         x.pmax[q] = m;
         hd->runmax = m;
+        hd->chains = (uint32_t)chains_s;
+        // the done part: pairs written (capped), or whether the whole words were written
+        const uint32_t dp = x.out[q].dpairs;
+        hd->ndone = !x.out[q].done ? 0u : dp ? (dirty_s < dp ? dirty_s : dp) : (dirty_s ? 1u : 0u);
+        hd->dwant = dirty_s;
+        if (x.pstat) x.pstat[kPsOut + q] = last_s[q];
+    }
+    if (threadIdx.x == 0 && x.dstat) {
+        // words left dirty past the pair capacity go out in a later round
+        bool left = false;
+        for (uint32_t p = 0; p < x.world; ++p)
+            if (p != x.rank && x.out[p].done && x.out[p].dpairs && dirty_s > x.out[p].dpairs) left = true;
+        x.dstat[kDstatLeft] = left ? 1u : 0u;
+        x.pstat[kPsDirty] = dirty_s;
     }
 }
 
@@ -1326,6 +1353,21 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
         a.total[applied] = (applied >= 1 ? a.total[applied - 1] : 0ull) + t;
         if (of) atomicOr(x.overflow, 1u);
     }
+    if (x.pstat && blockIdx.x == 0 && threadIdx.x < x.world) {  // full gossip: the next plans' inputs
+        const uint32_t q = threadIdx.x;
+        if (q == 0) {  // every rank's chains of the round
+            unsigned long long c = *x.self_chains;
+            for (uint32_t p = 0; p < x.world; ++p)
+                if (p != x.rank) c += x.in[p].hdr->chains;
+            *reinterpret_cast<unsigned long long*>(x.pstat + kPsChains) = c;
+        }
+        if (q != x.rank) {  // the largest sub-segment peer q sent and its dirty done words
+            uint32_t m = 0;
+            for (uint32_t s = 0; s < kSub; ++s) m = max(m, x.in[q].hdr->nlinks[s]);
+            x.pstat[kPsIn + q] = m;
+            x.pstat[kPsDwIn + q] = x.in[q].hdr->dwant;
+        }
+    }
     // Quiet-tail marks (push-sum): when F(applied) marked the segments with work in
     // the next round (the count after the round before it reached act_thr), the segment of every
     // actor of this rank that a remote message reaches is marked here, with F(applied)'s tag.
@@ -1359,15 +1401,30 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
     // range that also holds a neighbour's actors, the first and the last, is merged with an atomic OR)
     if (full && gossip && a.dbits && applied >= 0) {
         for (uint32_t q = 0; q < x.world; ++q) {
-            // a peer none of whose actors reported in the round changed no word (and sent none:
-            // k_shard_done_out skips such a round)
-            if (q == x.rank || !x.in[q].done || x.in[q].hdr->newly == 0ull) continue;
+            // a peer whose words all match what it shipped before sent none (ndone 0: k_shard_done_out
+            // skips such a round)
+            if (q == x.rank || !x.in[q].done) continue;
+            const uint32_t nd = x.in[q].hdr->ndone;
+            if (!nd) continue;
             const uint32_t w0 = x.abnd[q] >> 5, nw = ((x.abnd[q + 1] - 1u) >> 5) - w0 + 1u;
-            for (uint32_t i = gtid; i < nw; i += gstride) {
-                const uint32_t w = w0 + i, val = x.in[q].done[i], old = a.dbits[w];
+            const uint32_t dp = x.in[q].dpairs, n = dp ? (nd < dp ? nd : dp) : nw;
+            for (uint32_t i = gtid; i < n; i += gstride) {
+                uint32_t w = w0 + i, val;
+                if (dp) {  // (global word index, word) pairs
+                    const uint2 pr = reinterpret_cast<const uint2*>(x.in[q].done)[i];
+                    w = pr.x;
+                    val = pr.y;
+                    if (w - w0 >= nw) {  // a corrupt chunk: reported, never written
+                        atomicOr(x.overflow, 2u);
+                        continue;
+                    }
+                } else {
+                    val = x.in[q].done[i];
+                }
+                const uint32_t old = a.dbits[w];
                 if ((old | val) == old) continue;  // nothing new (most words, most rounds)
                 uint32_t now = val;
-                if (i == 0 || i + 1 == nw) now = atomicOr(&a.dbits[w], val) | val;
+                if (w == w0 || w + 1 == w0 + nw) now = atomicOr(&a.dbits[w], val) | val;
                 else a.dbits[w] = val;
                 // the summary bit of a word that just filled (one atomic per such word, not per round)
                 if (a.dsum && now == ~0u) atomicOr(&a.dsum[w >> 5], 1u << (w & 31u));
@@ -1781,6 +1838,8 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
 // atomic (k_shard_unpack): the filter program.fs:92 applies there exactly.
 __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
     const uint32_t r = a.r;
+    // the chain ring slot round r + 2 adds into (the pack of round r - 2, its last reader, has run)
+    if (a.cparts && blockIdx.x == 0 && threadIdx.x < 64) *part_slot(a.cparts, r + 2u, threadIdx.x) = 0u;
     unsigned long long prev = 0;
     if (r) prev = gate_count(a, (long long)r - 1);
     if (r && prev >= a.target) return;
@@ -1792,7 +1851,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
     const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;
     uint32_t q, end, step;
     node_range(q0, q1, span4, q, end, step);
-    uint32_t newly = 0;
+    uint32_t newly = 0, chains = 0;
     // block-uniform trip count: block_reserve synchronises the block; lanes past the end idle
     for (; q - threadIdx.x < end; q += step) {
         const bool valid = q < end;
@@ -1817,6 +1876,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
         for (uint32_t j = 0; j < 4; ++j) {
             const uint32_t v = v0 + j, tok = ((mine >> j) & 1u) ? (st4 >> (8u * j)) & 3u : 0u;
             uint32_t u[2] = {0u, 0u};
+            chains += tok;
             if (tok) {
                 const uint4 px = philox(v, r, kStreamGossip, a.seed);
                 const uint32_t t0 = scale_draw(px.x, a.nodes), t1 = scale_draw(px.y, a.nodes);
@@ -1869,20 +1929,51 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
         }
     }
     if (r) block_add(newly, a.parts, (long long)r - 1);
+    if (a.cparts) {  // the chains of round r: they size the next rounds' exchange (gp_api.cpp gs_cap)
+        __syncthreads();  // block_add's LDS slots are reused
+        block_add(chains, a.cparts, r);
+    }
 }
 
 // Full gossip on shards: this rank's words of the done bitmap (after F(r)) into every peer's chunk.
+// The peers' replicas only feed the sender-side filter, which stays exact however stale they are
+// (done only turns on; the receiver filters exactly), so words are shipped lazily: a word goes out
+// when it differs from what was last shipped (x.dship).  The plan's done part is either every word
+// of the range (dpairs 0: the receivers read them all when any changed) or up to dpairs (index,
+// word) pairs; words past that capacity stay dirty for a later round (x.dstat backlog flag).  Every
+// peer gets the same words.
 __global__ __launch_bounds__(kBlock) void k_shard_done_out(RoundArgs a, Xchg x) {
     if (applied_converged(a)) return;  // block-uniform
-    // none of this rank's actors reported in the round F(r) applied: no word changed, and the
-    // receivers skip the words (its header's count is 0); the early rounds of a run
+    // none of this rank's actors reported in the round F(r) applied and no word is left over: no word
+    // differs from what was shipped (the early rounds of a run); the header's counts stay 0
     const uint32_t newly = a.r ? wave_sum(*part_slot(a.parts, (long long)a.r - 1, threadIdx.x & 63u)) : 0u;
-    if (!newly) return;  // uniform: every wave sums the same final sub-counters
+    if (!newly && !x.dstat[kDstatLeft]) return;  // uniform: every wave sums the same final sub-counters
+    uint32_t dp = 0;
+    bool any = false;
+    for (uint32_t q = 0; q < x.world && !any; ++q)
+        if (q != x.rank && x.out[q].done) {
+            dp = x.out[q].dpairs;  // the sender's plan: the same for every peer
+            any = true;
+        }
+    if (!any) return;
     const uint32_t w0 = a.lo >> 5, nw = ((a.hi - 1u) >> 5) - w0 + 1u;
-    for (uint32_t q = 0; q < x.world; ++q) {
-        if (q == x.rank || !x.out[q].done) continue;
-        uint32_t* o = x.out[q].done;
-        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nw; i += gridDim.x * kBlock) o[i] = a.dbits[w0 + i];
+    // block-uniform trip count: every thread reaches block_reserve1
+    for (uint32_t base = blockIdx.x * kBlock; base < nw; base += gridDim.x * kBlock) {
+        const uint32_t i = base + threadIdx.x;
+        const bool valid = i < nw;
+        const uint32_t val = valid ? a.dbits[w0 + i] : 0u;
+        const bool dirty = valid && val != x.dship[w0 + i];
+        const uint32_t pos = block_reserve1(&x.dstat[kDstatCount], dirty);
+        if (!dp) {  // every word
+            if (valid)
+                for (uint32_t q = 0; q < x.world; ++q)
+                    if (q != x.rank && x.out[q].done) x.out[q].done[i] = val;
+            if (dirty) x.dship[w0 + i] = val;
+        } else if (dirty && pos < dp) {
+            for (uint32_t q = 0; q < x.world; ++q)
+                if (q != x.rank && x.out[q].done) reinterpret_cast<uint2*>(x.out[q].done)[pos] = make_uint2(w0 + i, val);
+            x.dship[w0 + i] = val;
+        }
     }
 }
 

@@ -73,6 +73,10 @@ class HipShard:
         self.rank, self.world = rank, world
         self.topology, self.algorithm = topology, algorithm
         self.lo, self.hi = int(self.shard.lo), int(self.shard.hi)
+        # full gossip sizes every round's chunks from the last round before a sync:
+        # its host loop syncs every 4 rounds, so the plans follow the run's activity (its receipts
+        # thin out by a third or more per round once targets report)
+        self.max_batch = 4 if (topology == "full" and algorithm == "gossip" and world > 1) else None
         self._plan()
         dev = torch.device("cuda", device)
         # buffers for the full plan (the first one); the caching allocator hands out 512-byte
@@ -83,18 +87,22 @@ class HipShard:
         self.status = _abi.Status()
 
     def _plan(self):
-        """The current per-peer chunk sizes (gp_shard_plan): they follow the activity of the run
-        (activity tiers) and are re-read after every sync."""
-        sb = np.zeros(self.world, np.int64)
-        rb = np.zeros(self.world, np.int64)
-        _abi.check(self.lib.gp_shard_plan(self.h, sb.ctypes.data_as(C.c_void_p), rb.ctypes.data_as(C.c_void_p)))
-        self.send_splits, self.recv_splits = [int(x) for x in sb], [int(x) for x in rb]
+        """The next round's per-peer chunk sizes (gp_shard_plan): they follow the activity of the
+        run (push-sum: per batch; full gossip: per round), so they are re-read after every round
+        and sync."""
+        if not hasattr(self, "_sb"):
+            self._sb = np.zeros(self.world, np.int64)
+            self._rb = np.zeros(self.world, np.int64)
+            self._sbp = self._sb.ctypes.data_as(C.c_void_p)
+            self._rbp = self._rb.ctypes.data_as(C.c_void_p)
+        _abi.check(self.lib.gp_shard_plan(self.h, self._sbp, self._rbp))
+        self.send_splits, self.recv_splits = self._sb.tolist(), self._rb.tolist()
 
     def shard_stats(self):
         s = _abi.ShardStats()
         _abi.check(self.lib.gp_shard_stats(self.h, C.byref(s)))
         return {"plan_changes": s.plan_changes, "restores": s.restores, "send_bytes": s.send_bytes,
-                "recv_bytes": s.recv_bytes, "restore_round": s.restore_round}
+                "recv_bytes": s.recv_bytes, "restore_round": s.restore_round, "bytes_sent": s.bytes_sent}
 
     @property
     def nodes(self) -> int:
@@ -106,6 +114,7 @@ class HipShard:
 
     def round(self):
         _abi.check(self.lib.gp_shard_round(self.h, C.c_void_p(self.send_buf.data_ptr())))
+        self._plan()  # this round's chunk sizes (the exchange that follows moves them)
 
     def deliver(self):
         _abi.check(self.lib.gp_shard_deliver(self.h, C.c_void_p(self.recv_buf.data_ptr())))
@@ -253,6 +262,8 @@ def run(engine, transport, max_rounds: int = 1 << 40, batch: int = 8, max_batch:
     """Advance this rank until the GLOBAL count reaches `nodes` (program.fs:49,56) or
     max_rounds rounds; every rank of the job must call it with the same arguments.  timer: a
     PhaseTimer (sampled per-phase event timing)."""
+    max_batch = _max_batch(engine, max_batch)
+    batch = min(batch, max_batch)
     st = engine.sync()
     goal = int(st.round) + max_rounds
     while not st.converged and st.round < goal:
@@ -280,6 +291,12 @@ def run(engine, transport, max_rounds: int = 1 << 40, batch: int = 8, max_batch:
     return st
 
 
+def _max_batch(engine, max_batch: int) -> int:
+    """The engine's own bound on rounds between syncs, if it has one (HipShard.max_batch)."""
+    own = getattr(engine, "max_batch", None)
+    return min(max_batch, own) if own else max_batch
+
+
 def _nodes(engine) -> int:
     return int(engine.layout.nodes)  # HipShard and the oracle's shard engine alike
 
@@ -289,13 +306,15 @@ def _next_batch(batch: int, max_batch: int, nodes: int, before: int, after: int)
     half-reported phase, where the activity tiers begin (the plan is chosen at every sync, and a
     short run such as full gossip would otherwise reach its end inside one long batch)."""
     if 2 * before < nodes <= 2 * after:
-        return 8
+        return min(8, max_batch)
     return min(batch * 2, max_batch)
 
 
 def run_local(engines, max_rounds: int = 1 << 40, batch: int = 8, max_batch: int = 64):
     """`run` for every shard of a job held in this process (LoopbackTransport)."""
     t = LoopbackTransport()
+    max_batch = _max_batch(engines[0], max_batch)
+    batch = min(batch, max_batch)
     sts = [e.sync() for e in engines]
     goal = int(sts[0].round) + max_rounds
     while not sts[0].converged and sts[0].round < goal:

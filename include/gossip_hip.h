@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 5
+#define GP_ABI_VERSION 6
 
 /* program.fs:151 "line", :191 "full", :227 "2D", :267 "Imp3D"; "3D" is build-defined (Q9) */
 enum gp_topology { GP_LINE = 0, GP_FULL = 1, GP_TWO_D = 2, GP_IMP3D = 3, GP_THREE_D = 4 };
@@ -54,10 +54,12 @@ enum gp_flags {
     GP_FLAG_GOSSIP_TALLY = 64, /* full gossip, one GPU: tally receipts by target bucket in every
                                   round from round 1 at any graph size (default: from 2^20 actors,
                                   after a round with many chains); a test hook, same results */
-    GP_FLAG_FULL_PLAN = 128,   /* push-sum shards: keep the full exchange plan (no activity tiers) */
-    GP_FLAG_TIGHT_TIERS = 256, /* push-sum shards: activity tiers from the first batch with no
-                                  headroom and a restore point at every sync, so reduced chunks
-                                  overflow and batches replay often; a test hook, same results */
+    GP_FLAG_FULL_PLAN = 128,   /* push-sum and full-gossip shards: keep the full exchange plan (no
+                                  activity tiers, no per-round plans) */
+    GP_FLAG_TIGHT_TIERS = 256, /* push-sum and full-gossip shards: sized plans from the first batch
+                                  with no headroom and a restore point at every sync, so reduced
+                                  chunks overflow and batches replay often (full gossip: done words
+                                  also wait for a later round); a test hook, same results */
 };
 
 typedef struct gp_config {
@@ -175,12 +177,17 @@ typedef struct gp_shard_layout {
  * topology, push-sum on line/2D/Imp3D/3D (push-sum on "full" is single-GPU only). */
 int gp_create_shard(const gp_config* cfg, int32_t rank, int32_t world, gp_layout* out,
                     gp_shard_layout* shard, void** handle);
-/* Per-peer byte counts of the current exchange (arrays of `world`; peer order): chunk p -> q is
+/* Per-peer byte counts of the next round's exchange (arrays of `world`; peer order): chunk p -> q is
  * sent_bytes[q] bytes at the running offset of the send buffer, and likewise for the receive
- * buffer.  The buffers are allocated for the full plan (gp_shard_layout send_total / recv_total);
- * push-sum shards size each batch's chunks from the activity of the batch before (activity tiers:
- * the converged tail ships a fraction of an all-sending round), so a host re-reads the plan after
- * every gp_shard_sync.  Both ends of a chunk always agree on its size. */
+ * buffer.  The buffers are allocated for the full plan (gp_shard_layout send_total / recv_total),
+ * and plans only shrink from it:
+ *   - push-sum shards size each batch's chunks from the activity of the batch before (activity
+ *     tiers: the converged tail ships a fraction of an all-sending round);
+ *   - full-gossip shards size every round's chunks (ABI 6): from the chain count, which at most
+ *     doubles per round, during the ramp, and from the last round's counts after it.
+ * The plan of round k holds from the gp_shard_deliver of round k-1 (or the gp_shard_sync / gp_reset
+ * before round k) to the gp_shard_deliver of round k, so a host reads it after every
+ * gp_shard_round.  Both ends of a chunk always agree on its size. */
 int gp_shard_plan(void* handle, int64_t* send_bytes, int64_t* recv_bytes);
 /* Enqueue one round on the handle's stream and pack what other ranks need into send_buf
  * (device memory, send_total bytes, 256-byte aligned).  Asynchronous. */
@@ -201,6 +208,8 @@ typedef struct gp_shard_counters {
     int64_t send_bytes;     /* bytes of the current plan's send / receive chunks                */
     int64_t recv_bytes;
     int64_t restore_round;  /* round of the current restore point (-1: none)                     */
+    int64_t bytes_sent;     /* exchange bytes this rank sent since the last reset, summed over the
+                               rounds packed (replayed rounds included) (ABI 6)                  */
 } gp_shard_counters;
 /* Exchange-plan counters of a shard (num_gpus > 1 handle: rank 0's). */
 int gp_shard_stats(void* handle, gp_shard_counters* out);

@@ -269,9 +269,52 @@ def test_full_gossip_tight_tiers_vs_oracle(n, world, seed):
         for e in engines:
             e.reset()
     if n >= 100000:
+        # sized plans overflow under tight tiers and the batches replay from restore points (the
+        # counts, states, pending receipts, the replica and the shipped done words)
         ss = [e.shard_stats() for e in engines]
         assert all(x["plan_changes"] > 0 for x in ss), ss
+        assert sum(x["restores"] for x in ss) > 0, ss
     for e in engines:
+        e.close()
+
+
+@pytest.mark.parametrize("n,world,seed", [(300000, 8, 6), (2000000, 8, 3), (1000000, 3, 9)])
+def test_full_gossip_round_plans(n, world, seed):
+    """Full gossip on shards sizes every round's chunks: through the ramp from the
+    chain bound (chains at most double per round), after it from the last round's counts, and the
+    done words as lazily shipped (index, word) pairs.  The run ships a fraction of the full plan's
+    bytes, replays nothing, and is bit-exact against the single-GPU engine and the full-plan shards."""
+    ref = Simulator(n, "full", "gossip", seed=seed)
+    rs = ref.step()
+    engines = _shards(n, "full", "gossip", world, seed)
+    full_bytes = int(engines[0].shard.send_total)
+    t = sharded.LoopbackTransport()
+    sts = [e.sync() for e in engines]
+    per_round, batch = [], 8
+    while not sts[0].converged:
+        for _ in range(batch):
+            for e in engines:
+                e.round()
+            per_round.append(sum(engines[0].send_splits))
+            t.exchange_all(engines)
+            for e in engines:
+                e.deliver()
+        sts = [e.sync() for e in engines]
+    assert (sts[0].round, sts[0].completed) == (rs.round, rs.completed)
+    _check_vs(ref, engines, "gossip")
+    ss = [e.shard_stats() for e in engines]
+    assert sum(x["restores"] for x in ss) == 0, ss
+    assert ss[0]["bytes_sent"] == sum(per_round)
+    assert per_round[0] < full_bytes / 20 and per_round[1] <= 2 * per_round[0] + 8192, per_round[:4]  # the ramp
+    assert sum(per_round) * 2 < len(per_round) * full_bytes, (sum(per_round), len(per_round), full_bytes)
+    # the same run with the full plan every round: the same counts
+    fp = _shards(n, "full", "gossip", world, seed, full_plan=True)
+    sharded.run_local(fp)
+    for a, b in zip(engines, fp):
+        np.testing.assert_array_equal(a.read_gossip()[0], b.read_gossip()[0])
+        np.testing.assert_array_equal(a.read_trace(), b.read_trace())
+        assert b.shard_stats()["bytes_sent"] > a.shard_stats()["bytes_sent"]
+    for e in engines + fp:
         e.close()
 
 
@@ -378,8 +421,9 @@ def test_shard_tables_scale_with_rank_count():
     for e in ranks:
         e.close()
     for b, o in zip(per, own):
-        # own share of the single-GPU bytes, x2 for rmsg / halos / chunks, and far below a global
-        # table of 16 B per actor
-        assert b < 2.0 * d1 * o / actors, (b, d1, o, actors)
+        # own share of the single-GPU bytes, x2.5 for rmsg / halos / chunks and the activity tiers'
+        # restore point (allocated at creation: ~35 B per own actor), and far below a global table of
+        # 16 B per actor
+        assert b < 2.5 * d1 * o / actors, (b, d1, o, actors)
         assert b < d1 / 2, (b, d1)
-    assert sum(per) < 2.0 * d1, (per, d1)
+    assert sum(per) < 2.5 * d1, (per, d1)

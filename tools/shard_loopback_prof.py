@@ -48,7 +48,9 @@ t = sharded.LoopbackTransport()
 events = []
 sts = [e.sync() for e in shards]
 send_bytes = [(0, sum(shards[0].send_splits))]
-batch = 8
+round_bytes = []  # rank 0's send bytes per round (full gossip plans every round)
+max_batch = sharded._max_batch(shards[0], 64)
+batch = min(8, max_batch)
 t0 = time.perf_counter()
 while not sts[0].converged and sts[0].round < cap:
     for _ in range(min(batch, cap - int(sts[0].round))):
@@ -60,6 +62,7 @@ while not sts[0].converged and sts[0].round < cap:
             e.round()
             if i == 0:
                 ev[1].record()
+        round_bytes.append(sum(shards[0].send_splits))  # rank 0's chunks of this round
         ev[2].record()
         t.exchange_all(shards)
         ev[3].record()
@@ -73,7 +76,7 @@ while not sts[0].converged and sts[0].round < cap:
     sts = [e.sync() for e in shards]
     assert len({(int(s.round), int(s.completed), int(s.converged)) for s in sts}) == 1, "shards disagree"
     send_bytes.append((int(sts[0].round), sum(shards[0].send_splits)))  # rank 0's plan from here on
-    batch = sharded._next_batch(batch, 64, nodes, before, int(sts[0].completed))  # the product loop's schedule
+    batch = sharded._next_batch(batch, max_batch, nodes, before, int(sts[0].completed))  # the product loop's schedule
 torch.cuda.synchronize()
 el = time.perf_counter() - t0
 rounds = int(sts[0].round)
@@ -119,7 +122,9 @@ summary = {
     "rank0_kernel": ks["kernel"], "rank0_kernel_avg_ms": ks["avg_ms"], "rank0_aux": ks["aux_kernel"],
     "rank0_aux_avg_ms": ks["aux_avg_ms"], "rank0_work_per_launch": ks["work_per_launch"],
     "rank0_actors": shards[0].hi - shards[0].lo,
-    "send_bytes_rank0_full_plan": send_bytes[0][1],
+    "send_bytes_rank0_full_plan": int(shards[0].shard.send_total),
+    "send_bytes_rank0_run": sum(round_bytes),  # every round packed, replays included
+    "send_bytes_rank0_if_full_plan": len(round_bytes) * int(shards[0].shard.send_total),
     "send_bytes_rank0_least": min(b for _, b in send_bytes),
     "shard_stats_rank0": shards[0].shard_stats(),
     "note": "all ranks serialised on one GPU; exchange = device copies (no RCCL); rank-round = round / world",
@@ -129,6 +134,6 @@ if a.series:
     with open(a.series, "w") as f:
         json.dump(dict(summary, per_round_ms=[round(x, 4) for x in per_round],
                        rank0_ms=[round(x, 4) for x in rank0], copies_ms=[round(x, 4) for x in copies],
-                       send_bytes=send_bytes, trace=trace), f)
+                       send_bytes=send_bytes, round_bytes=round_bytes, trace=trace), f)
 for e in shards:
     e.close()
