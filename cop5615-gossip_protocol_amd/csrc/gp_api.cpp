@@ -22,10 +22,7 @@ constexpr uint32_t kDsumMinActors = 1u << 25;  // the summary is used from here 
 // 10M +2% (profiles/round3/c4_scatter/cli_tally_thr.txt).
 constexpr size_t kTallyMinActors = 1u << 20;
 // Small Imp3D push-sum graphs on one GPU (no quiet marks): link senders also write their message into
-// the receiver's CSR slot (k_ps_pull<3>; A/B knob)
-#ifndef GP_SLOT_MSGS
-#define GP_SLOT_MSGS 1
-#endif
+// the receiver's CSR slot (k_ps_pull<3>)
 constexpr uint32_t kSlotMsgMaxActors = 1u << 18;
 #ifndef GP_TALLY_THR_DIV
 #define GP_TALLY_THR_DIV 8
@@ -432,7 +429,7 @@ int build_links(Handle* h) {
         // (one GPU: up to 2^18 actors; at 1M actors the scattered 16-byte slot stores cost more than
         // the load level they save, profiles/round4/small_imp3d)
         const bool slot_msgs = (h->sharded && h->world > 1) ||
-                               (!h->sharded && !h->act[0] && GP_SLOT_MSGS && h->g.actors < kSlotMsgMaxActors);
+                               (!h->sharded && !h->act[0] && h->g.actors < kSlotMsgMaxActors);
         if (slot_msgs && !h->gossip &&
             ((rc = h->alloc(&h->rmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->rmsg[1], (size_t)nsl, slo))))
             return rc;
@@ -740,10 +737,7 @@ constexpr int64_t kTimeEvery = 8;  // kernel timing: one round in 8
 // Kernel timing without a pass after the round kernel: one event pair per group of kTimeGroup
 // consecutive rounds.  Each record stalls the queue: groups of 8 added 9.3 ms to a 129 ms C3
 // run (7%, and 40% of a 20 us tail round); groups of 64 add about 1/8 of that (round 3).
-#ifndef GP_TIME_GROUP
-#define GP_TIME_GROUP 256  // = the largest batch: one event pair per batch (round 4; 64 before)
-#endif
-constexpr int64_t kTimeGroup = GP_TIME_GROUP;
+constexpr int64_t kTimeGroup = 256;  // = the largest batch: one event pair per batch (round 4; 64 before)
 #ifndef GP_TAIL_BATCH
 #define GP_TAIL_BATCH 32
 #endif
@@ -1680,8 +1674,13 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
                 if ((rc = h->alloc(&t.cnt, nc)) || (rc = h->alloc(&t.off, nc + 1)) || (rc = h->alloc(&t.tgt, 2 * n)) ||
                     (rc = h->alloc(&t.scratch, scan_scratch_words((uint32_t)nc))) ||
                     (rc = h->alloc(&t.chains, (size_t)kPartRing * kParts * kPartStride)) || (rc = h->alloc(&t.on, 4)) ||
-                    (GP_TALLY_INC16 && (rc = h->alloc(&t.inc16, (n + 7) & ~(size_t)7))))
+                    (rc = h->alloc(&t.inc16, (n + 7) & ~(size_t)7)))
                     return bail(rc);
+                // the live fallbacks, forced by a test hook: every count through the 32-bit words, and
+                // the counted-batch placement everywhere
+                const bool fb = (cfg->flags & GP_FLAG_TALLY_FALLBACKS) != 0;
+                t.esc = fb ? 1u : 0xFFFFu;
+                t.onepass = fb ? 0u : 1u;
             }
         } else if ((rc = h->alloc(&h->dir[0], xn, xlo)) || (rc = h->alloc(&h->dir[1], xn, xlo))) {
             return bail(rc);

@@ -1,6 +1,5 @@
 // gp_kernels.h — parameter blocks and launchers of the gfx950 round kernels (gp_kernels.hip).
 #pragma once
-#include <type_traits>
 #include "gp_common.h"
 
 namespace gp {
@@ -38,11 +37,8 @@ constexpr uint32_t kPsChains = 0, kPsDirty = 2, kPsOut = 16, kPsIn = 32, kPsDwIn
 static_assert(kPsOut + kMaxWorld <= kPsIn && kPsDwIn + kMaxWorld <= kPstatWords, "pstat layout");
 
 // Single-GPU Imp3D push-sum: the round kernel writes the link marks of its own messages (no
-// k_link_count pass; 1% faster than the separate pass at 10M).  GP_FUSE_LINK=0: the pass.
-#ifndef GP_FUSE_LINK
-#define GP_FUSE_LINK 1
-#endif
-constexpr bool kFuseLinkMarks = GP_FUSE_LINK != 0;
+// k_link_count pass; 1% faster than the separate pass at 10M).
+constexpr bool kFuseLinkMarks = true;
 
 // Push-sum link-slot marks carry their round: the pass after F(r) writes link_tag(r) into the
 // CSR slot of every actor whose round-r message took its extra link, into the array of parity
@@ -219,15 +215,13 @@ struct Launch {
 int grid_for(uint32_t n);
 uint32_t span_for(uint32_t n, int grid);
 
-// Quiet-wave marks: one byte per segment of kActSeg actors (GP_ACT_SEG: 4, 8, 16, 32, or 64 = one
-// wave).  4: C3 -8%, 100M -4% against 16 (profiles/round3/tail_ab); one mark per actor with
-// 1024-actor compaction was slower than 4 (scattered actors cost their own lines).
-#ifndef GP_ACT_SEG
-#define GP_ACT_SEG 4
-#endif
-constexpr uint32_t kActSeg = GP_ACT_SEG;
-constexpr uint32_t kActShift = kActSeg == 64u ? 6u : kActSeg == 32u ? 5u : kActSeg == 16u ? 4u : kActSeg == 8u ? 3u : 2u;
-static_assert((1u << kActShift) == kActSeg, "GP_ACT_SEG: 4, 8, 16, 32 or 64");
+// Quiet-wave marks: one byte per segment of kActSeg actors.  4: C3 -8%, 100M -4% against 16
+// (profiles/round3/tail_ab); one mark per actor with 1024-actor compaction was slower than 4
+// (scattered actors cost their own lines).  The compacted walk lists 64 / kActSeg segments per pass
+// (a power of two below 64: k_ps_quiet's tail walk).
+constexpr uint32_t kActShift = 2;
+constexpr uint32_t kActSeg = 1u << kActShift;
+static_assert(kActSeg >= 2u && kActSeg < 64u, "segments of 2 .. 32 actors");
 
 // round kernels
 void launch_ps_pull(const RoundArgs& a, const Launch& l, const Xchg* x = nullptr);  // x: a shard of several ranks
@@ -246,31 +240,30 @@ void launch_gs_push(const RoundArgs& a, const Launch& l);
 // scatter of the receipts by bucket (the draws recomputed) and an LDS tally per bucket then write
 // inc_cur whole.  Receipts to done targets are not filtered there (the receiver drops them).
 constexpr uint32_t kTallyShift = 15;          // 32768 targets per bucket: 128 KB of LDS counters
-#ifndef GP_TALLY_U16
-#define GP_TALLY_U16 1
-#endif
-typedef std::conditional<GP_TALLY_U16 != 0, uint16_t, uint32_t>::type TallyTarget;
+typedef uint16_t TallyTarget;                 // a placed receipt: its target's offset in the bucket
 constexpr uint32_t kMaxTallyBuckets = 4096;   // k_gs_full4's LDS counters: 16 KB at most
 #ifndef GP_TALLY_LATE_DIV
 #define GP_TALLY_LATE_DIV 64  // A/B knob; 0: no late tally
-#endif
-#ifndef GP_TALLY_INC16
-#define GP_TALLY_INC16 1  // A/B knob; 0: tallied rounds write the 32-bit receipt words
 #endif
 constexpr uint64_t kTallyLateDiv = GP_TALLY_LATE_DIV;  // also tally (filter on) while >= 1/64 of the nodes are not done
 struct GsTally {
     uint32_t* cnt;     // [nb * W] receipts per (bucket, workgroup), bucket-major; null: no tally
     uint32_t* off;     // [nb * W + 1] exclusive scan of cnt
     TallyTarget* tgt;  // receipts grouped by bucket (2 per actor at most): the target's offset in
-                       // its bucket (16 bits: 32768 targets per bucket; A/B knob GP_TALLY_U16)
+                       // its bucket (16 bits: 32768 targets per bucket)
     uint32_t* scratch; // scan scratch (scan_scratch_words(nb * W))
     uint32_t* chains;  // [4][kParts * kPartStride]: chains emitted in round r, ring slot r & 3
     uint32_t* on;      // [4]: round r tallies (written by block 0 of F(r))
-    uint16_t* inc16;   // [actors] receipts of the last tallied round (GP_TALLY_INC16); 0xFFFF: the
-                       // count is in that round's 32-bit receipt word
+    uint16_t* inc16;   // [actors] receipts of the last tallied round; a word holding esc: the count
+                       // is in that round's 32-bit receipt word
     uint32_t thr;      // tally in round r >= 1 when round r - 1 emitted at least thr chains to
                        // targets not done yet (estimated from the share of nodes not done)
     uint32_t nb, W;    // buckets; k_gs_full4's grid
+    // the live fallbacks (GP_FLAG_TALLY_FALLBACKS forces both; the same results either way):
+    uint32_t esc;      // 16-bit receipt words escape to the 32-bit word from this count on (0xFFFF;
+                       // the test hook: 1, every nonzero count)
+    uint32_t onepass;  // the placement draws once when a workgroup's receipts fit LDS (1), else in
+                       // counted batches (the test hook: 0, counted batches everywhere)
 };
 void launch_gs_full4(const RoundArgs& a, const GsTally& t, const Launch& l);  // full gossip, one GPU (lo == 0)
 // full gossip on shards: this rank's done-bitmap words into every peer's chunk (after F(k))

@@ -245,25 +245,15 @@ __device__ __forceinline__ T load_sel(const T* base, bool pred, uint32_t idx, ui
 }
 
 // The message loads of lanes without a grid hit / fired link read one row shared by the whole
-// grid (msg_prev[lo], 1) rather than the actor's own row (0, A/B knob): a wave's predicated-off
-// lanes then touch one line instead of eight, and a converged actor, which never reads its own
-// row, no longer pulls it in (all-sending C3 round 195.5 -> 189.8 us, profiles/round3/fallback_ab).
-#ifndef GP_MSG_FALLBACK_LO
-#define GP_MSG_FALLBACK_LO 1
-#endif
-constexpr bool kMsgFallbackLo = GP_MSG_FALLBACK_LO != 0;
+// grid (msg_prev[lo]) rather than the actor's own row: a wave's predicated-off lanes then touch one
+// line instead of eight, and a converged actor, which never reads its own row, no longer pulls it
+// in (all-sending C3 round 195.5 -> 189.8 us, profiles/round3/fallback_ab).
 
 // Link slots scanned with unrolled loads before the (rare) tail loop.
 #ifndef GP_LINK_UNROLL
 #define GP_LINK_UNROLL 4
 #endif
 constexpr uint32_t kLinkUnroll = GP_LINK_UNROLL;
-// A converged actor's held-row load as a branch-free load of one shared row (1) or an
-// exec-masked load under a branch (0, A/B knob): C3 -1% (profiles/round3/held_ab).
-#ifndef GP_HELD_SEL
-#define GP_HELD_SEL 1
-#endif
-constexpr bool kHeldSel = GP_HELD_SEL != 0;
 // Message loads issued for an actor's first GP_GRID_LOADS grid hits (A/B knob); later hits are
 // loaded on demand.  2 instead of 3: neutral (profiles/round3/held_ab).
 #ifndef GP_GRID_LOADS
@@ -279,40 +269,13 @@ static_assert(kGridLoads >= 1 && kGridLoads <= 6, "GP_GRID_LOADS: 1 .. 6");
 #define GP_FIRED_LOADS 1
 #endif
 constexpr uint32_t kFiredLoads = GP_FIRED_LOADS;
-// A/B knob: the shard round kernel (LM 2) loads fired links the same way (1) or per slot (0).
-#ifndef GP_FIRED_SHARDS
-#define GP_FIRED_SHARDS 0
-#endif
-constexpr bool kFiredShards = GP_FIRED_SHARDS != 0;
 
-// Timing-only builds (tools/variants) may drop parts of the round kernel to price them; the
-// product is built with 0, and the results of any other value are wrong by construction.
-// bit 0: no extra-link collect; bit 3: no Philox draw; bit 4: no grid-hit messages; bit 5: full
-// gossip receipts as plain random stores instead of atomics.
-// Stream attribution (push-sum round kernel): the load still issues, at an index folded into a
-// 4096-element, cache-resident prefix of its array, so the stream's HBM lines drop out while the
-// instruction mix stays: bit 6 held row, 7 the six neighbours' direction bytes, 8 flags, 9 CSR
-// offsets (li = v, nl = 1 instead), 10 CSR sources, 11 link marks, 12 lpos, 13 fired-link
-// message gathers, 14 grid-hit message gathers, 15 only the +-G^2 grid-hit gathers, 16 only the
-// +-G^2 direction bytes, 17 a link slot counts as fired iff its source id is 0 mod 7 (the
-// fired-link gathers keep their count without reading the marks), 18 the sender's link mark
-// stored into the cache-resident prefix, 19 no loads of the 3rd / 4th link message (the 16-byte
-// load instructions themselves), 20 no load of the 3rd grid-hit message, 21 no loads of the 3rd / 4th CSR source and mark.
-#ifndef GP_ABLATE
-#define GP_ABLATE 0
-#endif
-constexpr uint32_t kAblate = GP_ABLATE;
-// The CSR offsets of v (rev_off[v], rev_off[v + 1]) as one 8-byte load, the four unrolled
-// slots' sources as one 16-byte load and their marks as two dwords (1), or one load per element
-// (0, A/B knob).  Dword-aligned 8- and 16-byte loads (and byte-aligned ones) return the right
-// bytes on gfx950 (tools/microbench/unaligned.hip).  1: C3 -5.9%, 100M -6.1%
-// (profiles/round3/csr_vec_ab).  The marks as one byte-aligned dword and the +-1 neighbours'
-// direction bytes as one dword at v - 1 as well: neutral (one-byte loads are cheap; the 16-byte
-// ones fill the texture data path).
-#ifndef GP_CSR_VEC
-#define GP_CSR_VEC 1
-#endif
-constexpr bool kCsrVec = GP_CSR_VEC != 0 && kAblate == 0;
+// The CSR offsets of v (rev_off[v], rev_off[v + 1]) are one 8-byte load, the four unrolled slots'
+// sources one 16-byte load and their marks two dwords (round 3: C3 -5.9%, 100M -6.1% against one
+// load per element, profiles/round3/csr_vec_ab).  Dword-aligned 8- and 16-byte loads (and
+// byte-aligned ones) return the right bytes on gfx950 (tools/microbench/unaligned.hip).  The marks
+// as one byte-aligned dword and the +-1 neighbours' direction bytes as one dword at v - 1 as well:
+// neutral (one-byte loads are cheap; the 16-byte ones fill the texture data path).
 // The quiet-wave round kernel's SGPR cap (GP_PSQ_SGPR, 0 = the compiler's choice).  A 256-thread
 // workgroup is admitted per CU only while 800 / (ceil(sgpr / 16) * 16 + 16) allows it
 // (MI355X_MICROARCH.md, residency): 106 SGPRs -> 6 workgroups, <= 96 -> 7, <= 80 -> 8.
@@ -328,38 +291,6 @@ constexpr bool kCsrVec = GP_CSR_VEC != 0 && kAblate == 0;
 #define GP_PSQ_SGPR_ATTR
 #endif
 
-template <uint32_t BIT>
-__device__ __forceinline__ uint32_t ab(uint32_t i) {
-    return (kAblate & BIT) ? (i & 0xFFFu) : i;
-}
-
-// A/B knob: the message as one 16-byte non-temporal store (1) or two 8-byte ones (0).
-#ifndef GP_NT16
-#define GP_NT16 0
-#endif
-constexpr bool kNtStore16 = GP_NT16 != 0;
-// A/B knob: a converged actor does not read its held (S,W) (1), or reads it like the others (0).
-#ifndef GP_SKIP_CONV_HELD
-#define GP_SKIP_CONV_HELD 1
-#endif
-constexpr bool kSkipConvHeld = GP_SKIP_CONV_HELD != 0;
-// A/B knob: the small-graph round kernel issues its first actor's level-1 loads before the gate
-// resolves (1), or after it (0).
-#ifndef GP_EARLY_LEVEL1
-#define GP_EARLY_LEVEL1 1
-#endif
-constexpr bool kEarlyLevel1 = GP_EARLY_LEVEL1 != 0;
-// A/B knob: with the early level 1, also load all six neighbours' messages and the held (S,W)
-// there (1), or only the hits' messages at level 2 (0).
-#ifndef GP_PRE_GRID
-#define GP_PRE_GRID 1
-#endif
-constexpr bool kPreGrid = GP_PRE_GRID != 0;
-// A/B knob: the small-graph round kernels add their completion counts per wave (1) or per block (0).
-#ifndef GP_WAVE_ADD
-#define GP_WAVE_ADD 1
-#endif
-constexpr bool kWaveAdd = GP_WAVE_ADD != 0;
 
 // Cache policy of the link-mark stores (one random byte per fired link; GP_MARK_POL, A/B knob: 0
 // plain, 1 non-temporal, 2 non-temporal up to kMarkNtNodes nodes) in the one-GPU round kernel.  The marks of a round are
@@ -390,14 +321,6 @@ __device__ __forceinline__ void mark_store(const RoundArgs& a, uint8_t* p, uint8
     } else {
         byte_store<0>(p, x);
     }
-}
-
-// One 16-byte non-temporal store of a message (the round's messages cannot stay in L2 until the
-// next round reads them; streaming them leaves L2 to the rows that are re-read now).
-[[maybe_unused]] __device__ __forceinline__ void nt_store16(double2* p, double2 x) {
-    typedef double d2v __attribute__((ext_vector_type(2)));
-    const d2v y = {x.x, x.y};
-    __builtin_nontemporal_store(y, reinterpret_cast<d2v*>(p));
 }
 
 // One actor's round (program.fs:119-143 after collecting the round r-1 messages to v).
@@ -432,38 +355,30 @@ template <int LM, bool PRE = false>
 __device__ __forceinline__ PsLevel1 ps_level1(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v) {
     PsLevel1 p;
     p.m = presence(g, v);
-    p.f = a.flags[ab<256u>(v)];
+    p.f = a.flags[v];
     p.held = make_double2((double)v, 1.0);
     p.li = 0;
     p.nl = 0;
     if (PRE || r) {  // PRE: unconditional (no join for the loaded registers; ps_finish ignores
                      // them in round 0, when the buffers hold no messages yet)
-        if (PRE || !kSkipConvHeld) p.held = a.msg_prev[ab<64u>(v)];
+        if (PRE) p.held = a.msg_prev[v];
 #pragma unroll
         for (uint32_t k = 0; k < 6; ++k) {
             const uint32_t u = slot_src(g, v, k);
-            const uint32_t i = (k == 0 || k == 5) ? ab<65536u>(ab<128u>(u)) : ab<128u>(u);
-            p.d[k] = load_sel(a.dir_prev, (p.m & slot_bit(k)) != 0u, i, ab<128u>(v));
+            const uint32_t i = (k == 0 || k == 5) ? u : u;
+            p.d[k] = load_sel(a.dir_prev, (p.m & slot_bit(k)) != 0u, i, v);
         }
         if constexpr (PRE) {
 #pragma unroll
             for (uint32_t k = 0; k < 6; ++k)
                 p.gm6[k] = load_sel(a.msg_prev, (p.m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
         }
-        if (LM) {
-            if (kAblate & 512u) {
-                p.li = v;
-                p.nl = 1u;
-            } else if constexpr (kCsrVec) {  // rev_off[v], rev_off[v + 1] in one 8-byte load
-                typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-                u2v o;
-                __builtin_memcpy(&o, &a.rev_off[v], sizeof o);
-                p.li = o.x;
-                p.nl = (kAblate & 1u) ? 0u : o.y - o.x;
-            } else {
-                p.li = a.rev_off[v];
-                p.nl = (kAblate & 1u) ? 0u : a.rev_off[v + 1] - p.li;
-            }
+        if (LM) {  // rev_off[v], rev_off[v + 1] in one 8-byte load
+            typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+            u2v o;
+            __builtin_memcpy(&o, &a.rev_off[v], sizeof o);
+            p.li = o.x;
+            p.nl = o.y - o.x;
         }
     }
     return p;
@@ -478,13 +393,12 @@ struct LinkSend {
     double2 msg;
 };
 
-template <int LM, bool PRE = false, bool FF = (LM == 1 || kFiredShards)>
+template <int LM, bool PRE = false, bool FF = (LM == 1)>
 __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
                                               const PsLevel1& p, bool mark, LinkSend* ls = nullptr) {
     const uint32_t m = p.m;
     if (!m) return 0;
-    const uint32_t code = (kAblate & 8u) ? kth_bit(m, v % popc(m))
-                                          : kth_bit(m, scale_draw(philox_x(v, r, kStreamPush, a.seed), popc(m)));
+    const uint32_t code = kth_bit(m, scale_draw(philox_x(v, r, kStreamPush, a.seed), popc(m)));
     uint8_t f = (uint8_t)p.f;
     double2 held = (PRE && !r) ? make_double2((double)v, 1.0) : p.held;
     double ss = 0.0, ww = 0.0;
@@ -495,7 +409,6 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
         uint32_t hits = 0;
 #pragma unroll
         for (uint32_t k = 0; k < 6; ++k) hits |= ((m & slot_bit(k)) && d[k] == slot_code(k)) ? 1u << k : 0u;
-        if (kAblate & 16u) hits = 0;
         // The first kGridLoads grid hits (slot order = ascending source id) and their sources
         // (none: above every bound), computed once for the loads and the merge.
         uint32_t gs[kGridLoads], rest = hits;
@@ -507,19 +420,12 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
         double2 gm[kGridLoads];
 #pragma unroll
         for (int j = 0; j < (int)kGridLoads; ++j)
-            gm[j] = (PRE || ((kAblate & 1048576u) && j == 2)) ? make_double2(0.0, 0.0)
-                        : load_sel(a.msg_prev, gs[j] != 0xFFFFFFFFu,
-                                   (gs[j] == v - g.plane || gs[j] == v + g.plane) ? ab<32768u>(ab<16384u>(gs[j]))
-                                                                                : ab<16384u>(gs[j]),
-                                   kMsgFallbackLo ? a.lo : v);
+            gm[j] = PRE ? make_double2(0.0, 0.0) : load_sel(a.msg_prev, gs[j] != 0xFFFFFFFFu, gs[j], a.lo);
         uint32_t pend = hits;  // PRE: grid hits not yet added
         // A converged actor only relays what arrives (program.fs:125-127): its held (S,W) and so
         // its message row are not read (more than half of the C3 run's actor-rounds).  Issued
         // with the second load level, when the flags byte has long arrived.
-        if constexpr (!PRE && kSkipConvHeld && kHeldSel)
-            held = load_sel(a.msg_prev, !(f & 16u), ab<64u>(v), a.lo);
-        else if (!PRE && kSkipConvHeld && !(f & 16u))
-            held = a.msg_prev[ab<64u>(v)];
+        if constexpr (!PRE) held = load_sel(a.msg_prev, !(f & 16u), v, a.lo);
         uint32_t gi = 0;
         auto add = [&](double2 mm) {
             ss += mm.x;
@@ -559,7 +465,8 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
             bool lk[kLinkUnroll];
             double2 lm[kLinkUnroll];
             uint8_t lc[kLinkUnroll];
-            if constexpr (kCsrVec && kLinkUnroll == 4) {
+            static_assert(kLinkUnroll == 4, "GP_LINK_UNROLL: the slots load as one 16-byte load");
+            {
                 // the four unrolled slots' sources as one 16-byte load and their marks as two
                 // aligned dwords (slots past nl belong to the next actors and are ignored; the
                 // arrays are padded past their last slot)
@@ -575,20 +482,11 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                 const uint32_t sh = 8u * (li & 3u);
 #pragma unroll
                 for (uint32_t k = 0; k < 4; ++k) lc[k] = (uint8_t)(m8 >> (sh + 8u * k));
-            } else {
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k)
-                    ls[k] = ((kAblate & 2097152u) && k >= 2u) ? li + k
-                                                              : load_sel(a.rev_src, k < nl, ab<1024u>(li + k), a.slot_lo);
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkUnroll; ++k)
-                    lc[k] = ((kAblate & 2097152u) && k >= 2u) ? (uint8_t)(li >> 3)
-                                                              : load_sel(a.lcnt_prev, k < nl, ab<2048u>(li + k), a.slot_lo);
             }
             // ---- level 3: the messages of the sources whose slot is marked
 #pragma unroll
             for (uint32_t k = 0; k < kLinkUnroll; ++k)
-                lk[k] = k < nl && ((kAblate & 131072u) ? ls[k] % 7u == 0u : lc[k] == a.tag_prev);  // round tags
+                lk[k] = k < nl && lc[k] == a.tag_prev;  // round tags
             if constexpr (LM != 0 && kFiredLoads < kLinkUnroll && FF) {
                 // load the messages of the first kFiredLoads FIRED slots only (about one slot in
                 // seven fires: 0.14 messages per actor), the rest on demand (rare).  A shard reads
@@ -599,7 +497,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) rest |= lk[k] ? 1u << k : 0u;
                 auto msg_of = [&](uint32_t k, uint32_t u) -> const double2* {
                     if (LM == 2 && (u < a.lo || u >= a.hi)) return a.rmsg_prev + (li + k);
-                    return a.msg_prev + ab<8192u>(u);
+                    return a.msg_prev + u;
                 };
                 uint32_t fs[kFiredLoads];
                 bool fv[kFiredLoads];
@@ -612,7 +510,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
 #pragma unroll
                     for (uint32_t q = 1; q < kLinkUnroll; ++q) u = k == q ? ls[q] : u;
                     fs[j] = u;
-                    fm[j] = *(fv[j] ? msg_of(k, u) : a.msg_prev + (kMsgFallbackLo ? a.lo : v));
+                    fm[j] = *(fv[j] ? msg_of(k, u) : a.msg_prev + (a.lo));
                     rest &= rest - 1u;
                 }
 #pragma unroll
@@ -639,9 +537,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                     } else if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
                         lm[k] = a.rmsg_prev[li + k];
                     } else {
-                        lm[k] = ((kAblate & 524288u) && k >= 2u)
-                                    ? make_double2(0.0, 0.0)
-                                    : load_sel(a.msg_prev, lk[k], ab<8192u>(ls[k]), kMsgFallbackLo ? a.lo : v);
+                        lm[k] = load_sel(a.msg_prev, lk[k], ls[k], a.lo);
                     }
                 }
 #pragma unroll
@@ -667,16 +563,12 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
     // reads them, and streaming them past it leaves L2 to the +-G, +-G^2 rows read now
     // (measured ~1.5% per round; non-temporal LOADS of the CSR were 7% slower)
     if (o.send) {
-        if constexpr (kNtStore16) {
-            nt_store16(&a.msg_cur[v], o.msg);
-        } else {
-            __builtin_nontemporal_store(o.msg.x, &a.msg_cur[v].x);
-            __builtin_nontemporal_store(o.msg.y, &a.msg_cur[v].y);
-        }
+        __builtin_nontemporal_store(o.msg.x, &a.msg_cur[v].x);
+        __builtin_nontemporal_store(o.msg.y, &a.msg_cur[v].y);
     }
     __builtin_nontemporal_store(o.send ? (uint8_t)code : kDirNone, &a.dir_cur[v]);
     if constexpr (LM == 1 && kFuseLinkMarks) {  // the link pass's mark, written by the sender
-        if (o.send && code == kDirLink) mark_store(a, &a.lcnt_cur[ab<262144u>(a.lpos[ab<4096u>(v)])], (uint8_t)a.tag_cur);
+        if (o.send && code == kDirLink) mark_store(a, &a.lcnt_cur[a.lpos[v]], (uint8_t)a.tag_cur);
     }
     if constexpr (LM == 3) {  // small graphs: the message into the receiver's slot too, and its mark
         if (o.send && code == kDirLink) {
@@ -704,7 +596,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
     return o.conv_now ? 1u : 0u;
 }
 
-template <int LM, bool FF = (LM == 1 || kFiredShards)>
+template <int LM, bool FF = (LM == 1)>
 __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
                                              bool mark = false, LinkSend* ls = nullptr) {
     return ps_finish<LM, false, FF>(a, g, r, v, ps_level1<LM>(a, g, r, v), mark, ls);
@@ -818,11 +710,11 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
     uint32_t newly = 0;
     uint32_t v, end, step;
     node_range(a.lo, a.hi, a.span, v, end, step);
-    if constexpr (!Q && LM != 2 && kEarlyLevel1) {
+    if constexpr (!Q && LM != 2) {
         // Small graphs (one GPU, no quiet waves): the round is one dependent chain of loads with
         // the gate at its head, so the first actor's level-1 loads are issued ahead of the gate's
         // and both wait together (a thread without an actor loads actor lo's and drops them).
-        PsLevel1 p = ps_level1<LM, kPreGrid>(a, g, r, v < end ? v : a.lo);
+        PsLevel1 p = ps_level1<LM, true>(a, g, r, v < end ? v : a.lo);
         const unsigned long long prev = gate_count_wave(a, a.r);
         if (prev >= a.target) return;
         // keep the uses of the level-1 bytes below the gate (hoisted above it, they would wait
@@ -830,17 +722,14 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
 #pragma unroll
         for (int k = 0; k < 6; ++k) asm volatile("" : "+v"(p.d[k]));
         asm volatile("" : "+v"(p.f));
-        if constexpr (kPreGrid) {
 #pragma unroll
-            for (int k = 0; k < 6; ++k) asm volatile("" : "+v"(p.gm6[k].x), "+v"(p.gm6[k].y));
-            asm volatile("" : "+v"(p.held.x), "+v"(p.held.y));
-        }
+        for (int k = 0; k < 6; ++k) asm volatile("" : "+v"(p.gm6[k].x), "+v"(p.gm6[k].y));
+        asm volatile("" : "+v"(p.held.x), "+v"(p.held.y));
         if (v < end) {
-            newly += ps_finish<LM, kPreGrid>(a, g, r, v, p, false);
+            newly += ps_finish<LM, true>(a, g, r, v, p, false);
             for (v += step; v < end; v += step) newly += ps_actor<LM>(a, g, r, v);
         }
-        if constexpr (kWaveAdd) wave_add(newly, a.parts, r);
-        else block_add(newly, a.parts, r);
+        wave_add(newly, a.parts, r);
         return;
     }
     // converged after round r - 1 (one GPU, small graphs: Q = false, the per-wave gate)
@@ -849,7 +738,7 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
     const bool mark = Q && prev >= a.act_thr;                          // F(r) marks round r + 1
     const bool skip = Q && r >= 2u && a.total[r - 2] >= a.act_thr;  // F(r - 1) marked round r
     const uint8_t tag = (uint8_t)a.tag_cur;  // link_tag(r)
-    if constexpr (Q && kActSeg < 64u) {
+    if constexpr (Q) {
         const bool tail = skip;  // block-uniform: the compacted segment walk of the run's tail
         TailWalk t = tail_walk(a, tail);
         uint32_t walked = 0;
@@ -864,7 +753,7 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
             }
             LinkSend ls;
             if (u - a.lo < a.hi - a.lo) {  // lo <= u < hi (a shard's edge segments)
-                newly += ps_actor<LM, LM == 1 || LM == 2 || kFiredShards>(a, g, r, u, mark, LM == 2 ? &ls : nullptr);
+                newly += ps_actor<LM, LM == 1 || LM == 2>(a, g, r, u, mark, LM == 2 ? &ls : nullptr);
                 ++walked;
             }
             if constexpr (LM == 2) {
@@ -886,13 +775,7 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
         if (a.work) block_add_u64(walked, a.work + (blockIdx.x & (kParts - 1)) * kWorkStride);
         return;
     }
-    for (; v < end; v += step) {
-        if (skip && a.act_prev[v >> kActShift] != tag) {  // wave-uniform: 64 consecutive actors
-            __builtin_nontemporal_store(kDirNone, &a.dir_cur[v]);
-            continue;
-        }
-        newly += ps_actor<LM>(a, g, r, v, mark);
-    }
+    for (; v < end; v += step) newly += ps_actor<LM>(a, g, r, v, false);
     block_add(newly, a.parts, r);
 }
 
@@ -1028,10 +911,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_pull(RoundArgs a) {
             newly += gs_actor<LINK, true>(a, g, r, v, p);
             for (v += step; v < end; v += step) newly += gs_actor<LINK, true>(a, g, r, v, gs_level1<LINK>(a, g, v));
         }
-        if (r) {
-            if constexpr (kWaveAdd) wave_add(newly, a.parts, (long long)r - 1);
-            else block_add(newly, a.parts, (long long)r - 1);
-        }
+        if (r) wave_add(newly, a.parts, (long long)r - 1);
     } else {
         if (r && gate(a, (long long)r - 1)) return;
         const GsLevel1 none{};
@@ -1537,21 +1417,16 @@ __device__ __forceinline__ void gs_push_body(const RoundArgs& a, const Xchg* xp)
                 const uint4 px = philox(v, r, kStreamGossip, a.seed);
                 const uint32_t t0 = generic_target(a, v, m, scale_draw(px.x, d));
                 const uint32_t t1 = tok > 1 ? generic_target(a, v, m, scale_draw(px.y, d)) : t0;
-                if constexpr (kAblate & 32u) {  // timing only: random plain stores for the atomics
-                    a.inc_cur[t0] = 1u;
-                    if (tok > 1) a.inc_cur[t1] = 1u;
-                } else {
-                    // The sender skips a target it sees done (program.fs:92), so ~2/3 of a run's
-                    // receipts never become atomics.  The byte it reads is the target's state
-                    // after round r-2 or r-1 (this kernel may have applied r-1 already); done
-                    // only ever turns on, so a target seen done is also done under the
-                    // receiver's filter (state after r-1), which drops the receipt anyway.
-                    const bool send1 = tok > 1;
-                    const uint8_t s0 = a.gstate[t0];
-                    const uint8_t s1 = send1 ? a.gstate[t1] : (uint8_t)4u;
-                    if (!(s0 & 4u)) atomicAdd(&a.inc_cur[t0], 1u);
-                    if (!(s1 & 4u)) atomicAdd(&a.inc_cur[t1], 1u);
-                }
+                // The sender skips a target it sees done (program.fs:92), so ~2/3 of a run's
+                // receipts never become atomics.  The byte it reads is the target's state after
+                // round r-2 or r-1 (this kernel may have applied r-1 already); done only ever turns
+                // on, so a target seen done is also done under the receiver's filter (state after
+                // r-1), which drops the receipt anyway.
+                const bool send1 = tok > 1;
+                const uint8_t s0 = a.gstate[t0];
+                const uint8_t s1 = send1 ? a.gstate[t1] : (uint8_t)4u;
+                if (!(s0 & 4u)) atomicAdd(&a.inc_cur[t0], 1u);
+                if (!(s1 & 4u)) atomicAdd(&a.inc_cur[t1], 1u);
             }
         } else {  // receipts for another rank's actors go to its send chunk (the target id)
             const Xchg& x = *xp;
@@ -1607,17 +1482,11 @@ __device__ __forceinline__ uint32_t tally_chains(const GsTally& t, uint32_t r) {
 
 // Column of k_gs_full4 workgroup w in cnt's rows (and its inverse).  Workgroups go round-robin to
 // the 8 XCDs, so w and w + 1 run on different L2s; columns grouped per XCD (W is a multiple of 8)
-// let one L2 write whole lines of a row.  Any column order serves: a bucket's segment is filled
-// in column order, and k_gs_tally_count tallies the segment whole.
-#ifndef GP_TALLY_COLXCD
-#define GP_TALLY_COLXCD 1  // A/B knob; 0: column = workgroup index
-#endif
-__device__ __forceinline__ uint32_t tally_col(uint32_t w, uint32_t W) {
-    return GP_TALLY_COLXCD ? (w & 7u) * (W >> 3) + (w >> 3) : w;
-}
-__device__ __forceinline__ uint32_t tally_wg(uint32_t c, uint32_t W) {
-    return GP_TALLY_COLXCD ? (c % (W >> 3)) * 8u + c / (W >> 3) : c;
-}
+// let one L2 write whole lines of a row (C4 46.36 -> 46.08 ms against column = workgroup index,
+// profiles/round4/tally_rows/colxcd_ab).  Any column order serves: a bucket's segment is filled in
+// column order, and k_gs_tally_count tallies the segment whole.
+__device__ __forceinline__ uint32_t tally_col(uint32_t w, uint32_t W) { return (w & 7u) * (W >> 3) + (w >> 3); }
+__device__ __forceinline__ uint32_t tally_wg(uint32_t c, uint32_t W) { return (c % (W >> 3)) * 8u + c / (W >> 3); }
 
 // The state bytes (st4) and the round r - 1 receipt words of actors v0 .. v0+3.  Deep in a run's
 // tail (deep: block-uniform) a quad of four done actors skips its receipt words: a done actor ignores
@@ -1627,14 +1496,10 @@ __device__ __forceinline__ uint32_t tally_wg(uint32_t c, uint32_t W) {
 #ifndef GP_DEEP_DIV
 #define GP_DEEP_DIV 64  // A/B knob: "deep" = fewer than 1/GP_DEEP_DIV of the nodes not done (0: off)
 #endif
-// i16: round r - 1 tallied into 16-bit words (k_gs_tally_count); kInc16Esc sends to the 32-bit word.
-#ifndef GP_INC16_ESC
-#define GP_INC16_ESC 0xFFFF  // test knob: 1 sends every nonzero count through the 32-bit words
-#endif
-constexpr uint32_t kInc16Esc = GP_INC16_ESC;
-// want: the receipt words were due (read).
+// i16: round r - 1 tallied into 16-bit words (k_gs_tally_count); a word holding esc sends to the
+// 32-bit word (GsTally::esc).  want: the receipt words were due (read).
 __device__ __forceinline__ uint4 load_quad(const RoundArgs& a, const uint16_t* i16, uint32_t v0, uint32_t r, bool deep,
-                                           uint32_t& st4, bool& want) {
+                                           uint32_t& st4, bool& want, uint32_t esc = 0xFFFFu) {
     uint4 in4 = make_uint4(0u, 0u, 0u, 0u);
     st4 = *reinterpret_cast<const uint32_t*>(a.gstate + v0);
     want = r && (!deep || (st4 & 0x04040404u) != 0x04040404u);
@@ -1642,10 +1507,10 @@ __device__ __forceinline__ uint4 load_quad(const RoundArgs& a, const uint16_t* i
         if (i16) {
             const uint2 h = *reinterpret_cast<const uint2*>(i16 + v0);
             in4 = make_uint4(h.x & 0xFFFFu, h.x >> 16, h.y & 0xFFFFu, h.y >> 16);
-            if (in4.x == kInc16Esc) in4.x = a.inc_prev[v0];
-            if (in4.y == kInc16Esc) in4.y = a.inc_prev[v0 + 1u];
-            if (in4.z == kInc16Esc) in4.z = a.inc_prev[v0 + 2u];
-            if (in4.w == kInc16Esc) in4.w = a.inc_prev[v0 + 3u];
+            if (in4.x == esc) in4.x = a.inc_prev[v0];
+            if (in4.y == esc) in4.y = a.inc_prev[v0 + 1u];
+            if (in4.z == esc) in4.z = a.inc_prev[v0 + 2u];
+            if (in4.w == esc) in4.w = a.inc_prev[v0 + 3u];
         } else {
             in4 = *reinterpret_cast<const uint4*>(a.inc_prev + v0);
         }
@@ -1688,9 +1553,6 @@ __device__ __forceinline__ uint32_t gs_apply4(const RoundArgs& a, uint32_t v0, u
     return st4;
 }
 
-#ifndef GP_GS_PREFETCH
-#define GP_GS_PREFETCH 0  // A/B knob: 1 loads the next quad before applying this one
-#endif
 __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
     extern __shared__ uint32_t tcnt[];  // tally rounds: receipts per target bucket (t.nb)
     const uint32_t r = a.r;
@@ -1709,7 +1571,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
     const bool tally = t.cnt && r >= 1u && t.on[r & 3u];
     // round r - 1 tallied: its receipts are in t.inc16, and its 32-bit words hold stale counts (the
     // round before a round that tallies leaves them unzeroed) but for the 0xFFFF escapes
-    const bool from16 = GP_TALLY_INC16 && t.cnt && r >= 2u && t.on[(r - 1u) & 3u];
+    const bool from16 = t.cnt && r >= 2u && t.on[(r - 1u) & 3u];
     const double ch = (t.cnt && r >= 1u) ? (double)tally_chains(t, r - 1u) : 0.0;  // (no tally: no chains array)
     const bool tally_next = t.cnt && r >= 1u && prev < a.target &&
                             (ch * (double)(a.target - prev) >= (double)t.thr * (double)a.target ||
@@ -1738,14 +1600,6 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
     node_range(0u, nq, span4, q, end, step);
     uint32_t newly = 0, chains = 0;
     const uint16_t* i16 = from16 ? t.inc16 : nullptr;
-#if GP_GS_PREFETCH
-    // the next quad's state and receipt words are loaded before this one is applied (only this lane
-    // touches them in this round)
-    uint32_t st_n = 0;
-    bool want_n = false;
-    uint4 in_n = make_uint4(0u, 0u, 0u, 0u);
-    if (q < end) in_n = load_quad(a, i16, q << 2, r, deep, st_n, want_n);
-#endif
     // uniform per wave: the 8 lanes sharing a bitmap word reduce together
     for (; q - (threadIdx.x & 63u) < end; q += step) {
         const bool valid = q < end;
@@ -1753,14 +1607,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
         uint32_t st4 = 0, done4 = 0;
         if (valid) {
             bool want;
-#if GP_GS_PREFETCH
-            uint4 in4 = in_n;
-            st4 = st_n;
-            want = want_n;
-            if (q + step < end) in_n = load_quad(a, i16, (q + step) << 2, r, deep, st_n, want_n);
-#else
-            uint4 in4 = load_quad(a, i16, v0, r, deep, st4, want);
-#endif
+            uint4 in4 = load_quad(a, i16, v0, r, deep, st4, want, t.esc);
             uint32_t inc[4] = {in4.x, in4.y, in4.z, in4.w};
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
@@ -2068,12 +1915,6 @@ __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t x, uint32_t* wsum
 // workgroup is dealt round-robin to the kScatK thread groups.  k_gs_tally_scatter stores each
 // receipt where its LDS position falls, one 4-byte store per line: its 98M receipts per C4 peak
 // round wrote 2.94 GB (7.5x the receipt bytes, profiles/round3/c4_tally/pmc_scatter.txt).
-#ifndef GP_SCAT_XCD
-#define GP_SCAT_XCD 1  // A/B knob; 0: column group = workgroup index
-#endif
-#ifndef GP_SCAT_ONEPASS
-#define GP_SCAT_ONEPASS 1  // A/B and test knob; 0: every workgroup in counted batches
-#endif
 constexpr uint32_t kScatK = 4;
 constexpr uint32_t kScatBlock = kScatK * kBlock;
 constexpr uint32_t kScatMaxPerIter = kScatBlock * 8u;  // 4 actors x 2 chains per thread
@@ -2090,7 +1931,7 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
     // XCDs), so the count and prefix lines they read, and the bucket segments they write next to
     // each other, meet in one L2
     const uint32_t G = W / kScatK;
-    const uint32_t sg = (GP_SCAT_XCD && (G & 7u) == 0u) ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    const uint32_t sg = (G & 7u) == 0u ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
     uint4 cw[4];  // receipts of buckets 4 * tid + j from workgroups kScatK*sg + 0..3 (x..w)
     {  // bucket starts: exclusive scan of k_tally_rows' row totals, 4 buckets per thread
         const uint32_t* tot = t.off + (size_t)nb * G;
@@ -2145,7 +1986,7 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
             s += v[j];
         }
         uint32_t run = block_excl_scan_n<kScatBlock>(s, misc + 16, &all);
-        if (GP_SCAT_ONEPASS && all <= cap) {  // one pass: starts from the counts
+        if (t.onepass && all <= cap) {  // one pass: starts from the counts
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j) {
                 const uint32_t b = 4u * tid + j;
@@ -2214,13 +2055,10 @@ __global__ __launch_bounds__(kScatBlock) void k_gs_tally_scatter_lds(RoundArgs a
 }
 
 // Tallied round: one workgroup per target bucket counts its receipts in LDS and writes the
-// bucket's whole range of t.inc16 (GP_TALLY_INC16; else of inc_cur), zeros included, so nothing is
-// left to clear.  Its 128 KB of LDS
-// admit one workgroup per CU: GP_COUNT_BLOCK threads (A/B knob) keep that many in flight.
-#ifndef GP_COUNT_BLOCK
-#define GP_COUNT_BLOCK 1024
-#endif
-constexpr uint32_t kCountBlock = GP_COUNT_BLOCK;
+// bucket's whole range of t.inc16, zeros included, so nothing is left to clear: 16-bit words (half
+// the bytes here and in F(r + 1); a count from t.esc up escapes to the 32-bit word).  Its 128 KB of
+// LDS admit one workgroup per CU: 1024 threads keep that many in flight.
+constexpr uint32_t kCountBlock = 1024;
 __global__ __launch_bounds__(kCountBlock) void k_gs_tally_count(RoundArgs a, GsTally t, const uint32_t* bst) {
     extern __shared__ uint32_t h[];
     if (!t.on[a.r & 3u]) return;  // uniform
@@ -2234,15 +2072,11 @@ __global__ __launch_bounds__(kCountBlock) void k_gs_tally_count(RoundArgs a, GsT
     __syncthreads();
     const uint32_t base = b << kTallyShift, na = a.hi;
     const uint32_t n = na - base < S ? na - base : S;
-    if (GP_TALLY_INC16) {  // 16-bit words (half the bytes here and in F(r + 1)); a count that does
-                           // not fit escapes to the 32-bit word
-        for (uint32_t i = threadIdx.x; i < n; i += kCountBlock) {
-            const uint32_t c = h[i];
-            t.inc16[base + i] = (uint16_t)(c < kInc16Esc ? c : kInc16Esc);
-            if (c >= kInc16Esc) a.inc_cur[base + i] = c;
-        }
-    } else {
-        for (uint32_t i = threadIdx.x; i < n; i += kCountBlock) a.inc_cur[base + i] = h[i];
+    const uint32_t esc = t.esc;
+    for (uint32_t i = threadIdx.x; i < n; i += kCountBlock) {
+        const uint32_t c = h[i];
+        t.inc16[base + i] = (uint16_t)(c < esc ? c : esc);
+        if (c >= esc) a.inc_cur[base + i] = c;
     }
 }
 
@@ -2548,12 +2382,6 @@ uint32_t span_for(uint32_t n, int grid) {
     return (s + kBlock - 1) / kBlock * kBlock;
 }
 
-// Dynamic LDS per workgroup that caps the round kernel's residency (A/B knob): 24 KB allows 6
-// workgroups (= 6 waves per SIMD) per CU's 160 KB whatever the VGPR count permits.
-#ifndef GP_PS_LDS_CAP
-#define GP_PS_LDS_CAP 0
-#endif
-
 // The quiet-wave kernel's grid: the workgroups resident at once (GP_PSQ_PER_CU per CU; 7 with the
 // SGPR cap), unless the node range needs fewer.
 #ifndef GP_PSQ_PER_CU
@@ -2562,7 +2390,7 @@ uint32_t span_for(uint32_t n, int grid) {
 static int quiet_grid(const Launch& l) { return l.grid < 256 * GP_PSQ_PER_CU ? l.grid : 256 * GP_PSQ_PER_CU; }
 
 void launch_ps_pull(const RoundArgs& a, const Launch& l, const Xchg* x) {
-    const unsigned lds = GP_PS_LDS_CAP;
+    constexpr unsigned lds = 0;
     const bool q = a.act_cur != nullptr;
     if (!a.g.has_link) {
         if (q) hipLaunchKernelGGL((k_ps_quiet<0>), dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a);
@@ -2606,10 +2434,8 @@ void launch_gs_full4(const RoundArgs& a, const GsTally& t, const Launch& l) {
     hipLaunchKernelGGL(k_gs_full4, dim3(t.cnt ? t.W : (uint32_t)l.grid), dim3(kBlock), lds, l.stream, a, t);
 }
 
-// Batched placement (k_gs_tally_scatter_lds, 1) or one store per receipt (0, A/B knob).
-#ifndef GP_SCATTER_LDS
-#define GP_SCATTER_LDS 1
-#endif
+// Batched placement (k_gs_tally_scatter_lds) where its 160 KB of LDS can be allowed, else one store
+// per receipt (k_gs_tally_scatter, after the full scan).
 constexpr uint32_t kScatLdsBytes = 160u * 1024u;  // one workgroup per CU
 bool g_scatter_lds = false;
 
@@ -2618,7 +2444,7 @@ int prepare_gs_tally() {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gs_tally_count), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)((1u << kTallyShift) * sizeof(uint32_t))) != hipSuccess)
         return -1;
-    g_scatter_lds = GP_SCATTER_LDS != 0 &&
+    g_scatter_lds =
                     hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gs_tally_scatter_lds),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScatLdsBytes) == hipSuccess;
     (void)hipGetLastError();

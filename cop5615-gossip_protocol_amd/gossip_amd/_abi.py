@@ -25,6 +25,7 @@ FLAG_QUIET_WAVES = 32
 FLAG_GOSSIP_TALLY = 64
 FLAG_FULL_PLAN = 128
 FLAG_TIGHT_TIERS = 256
+FLAG_TALLY_FALLBACKS = 512
 ERRORS = {-1: "GP_EINVAL", -2: "GP_ENOMEM", -3: "GP_EHIP", -4: "GP_ESTATE", -5: "GP_EOVERFLOW", -6: "GP_ERCCL"}
 
 

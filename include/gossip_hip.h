@@ -60,6 +60,11 @@ enum gp_flags {
                                   with no headroom and a restore point at every sync, so reduced
                                   chunks overflow and batches replay often (full gossip: done words
                                   also wait for a later round); a test hook, same results */
+    GP_FLAG_TALLY_FALLBACKS = 512, /* full gossip, one GPU, receipt tally: run the paths a large
+                                  graph takes only at extreme counts, everywhere: the counted-batch
+                                  placement (a workgroup's receipts past its LDS) and the 32-bit
+                                  escape of the 16-bit receipt words (counts >= 0xFFFF); a test
+                                  hook, same results */
 };
 
 typedef struct gp_config {

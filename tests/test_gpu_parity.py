@@ -302,3 +302,22 @@ def test_full_gossip_tally_vs_oracle(n, seed):
     np.testing.assert_array_equal(gpu.read_trace(), cpu.read_trace())
     gpu.close()
     cpu.close()
+
+
+@pytest.mark.parametrize("n,seed,forced", [(1_200_000, 4, True), (10_000_000, 1, False)])
+def test_full_gossip_tally_fallbacks_vs_oracle(n, seed, forced):
+    """The tally's live fallbacks, which a large graph reaches only at extreme counts, forced in every
+    tallied round (GP_FLAG_TALLY_FALLBACKS): the counted-batch placement (a workgroup whose receipts
+    outgrow its LDS; at C4 a workgroup peaks at ~24K receipts against room for 34.8K) and the 32-bit
+    escape of the 16-bit receipt words (counts >= 0xFFFF), every nonzero count through it.  C4-shaped
+    runs (1.2M forced from round 1; 10M with the default tally rule), bit for bit against the oracle."""
+    gpu = Simulator(n, "full", "gossip", seed=seed, gossip_tally=forced, tally_fallbacks=True)
+    cpu = oracle.OracleSim(n, "full", "gossip", seed=seed)
+    gs = gpu.step()
+    cs = cpu.step(threads=16)
+    assert gs.converged and (gs.round, gs.completed) == (cs.round, cs.completed)
+    np.testing.assert_array_equal(gpu.read_trace(), cpu.read_trace())
+    check_same(gpu, cpu, "gossip")
+    assert gpu.kernel_stats()["kernel"] == "k_gs_full4+tally"  # the tally was built for this graph
+    gpu.close()
+    cpu.close()
