@@ -447,8 +447,9 @@ def main(argv=None):
     if use_shards:  # one extra, untimed step with sampled per-phase events (rank 0 reports)
         timer = sharded.PhaseTimer()
         one_step(timer)
-        per_rank = dict(timer.means(), actors=own, bytes_sent_per_round=sum(eng.send_splits),
-                        bytes_received_per_round=sum(eng.recv_splits), world=world)
+        sent, received = eng.bytes_per_round()
+        per_rank = dict(timer.means(), actors=own, bytes_sent_per_round=sent, bytes_received_per_round=received,
+                        world=world, pieces=eng.npieces)
     out = None
     if rank == 0:
         cpu = None

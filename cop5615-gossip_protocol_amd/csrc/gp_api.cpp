@@ -14,6 +14,8 @@
 #define GP_ACT_PCT 99
 #endif
 constexpr uint32_t kQuietMinActors = 1u << 20;
+// Shards run their rounds in pieces from this many actors on every rank (GP_FLAG_PIECES).
+constexpr int64_t kPieceMinActors = 1 << 20;
 // Full gossip done bitmap: one bit per actor, then its summary (one bit per 32-actor word).
 constexpr uint32_t kDsumMinActors = 1u << 25;  // the summary is used from here (dbits > an L2)
 // Full gossip on one GPU: the receipt tally (gp_kernels.h GsTally) is built from this many actors
@@ -150,13 +152,21 @@ struct Handle {
     uint32_t lo = 0, hi = 0;
     uint32_t halo = 0;  // z-plane (Imp3D/3D) or 1 actor (line/2D) exchanged with rank +-1
     std::vector<int64_t> abnd, sbnd;          // actor / link-slot bounds of every rank
-    std::vector<unsigned long long> lhist;    // (src rank, dst rank, degree) link counts
-    std::vector<Chunk> out_chunk, in_chunk;   // per peer
+    // A round in pieces: piece i of every rank's range is computed, packed and
+    // exchanged on its own, so the exchange of one piece overlaps the next piece's kernels.  Chunks
+    // are per (piece, peer), index i * world + q, laid out piece-major in the buffers.
+    int npiece = 1;
+    std::vector<int64_t> pbnd;                // piece bounds of every rank: pbnd[q * (npiece + 1) + i]
+    int piece_next = 0;                       // the next piece gp_shard_round_piece packs
+    int64_t round_slot = -1;                  // timing slot of the round being packed (-1: untimed)
+    std::vector<unsigned long long> lhist;    // (src piece, dst rank, degree) link counts
+    std::vector<Chunk> out_chunk, in_chunk;   // per (piece, peer)
     std::vector<int64_t> out_off, in_off;     // chunk offsets inside the send / recv buffers
+    std::vector<int64_t> out_poff, in_poff;   // each piece's region (npiece + 1 offsets)
     int64_t send_total = 0, recv_total = 0;
-    uint32_t max_in_cap = 0;
+    std::vector<uint32_t> max_in_cap;         // per piece
     std::vector<Chunk> full_out, full_in;  // the full plan (the buffers are sized for it)
-    uint32_t* pmax = nullptr;      // running max of link entries per sub-segment to each peer
+    uint32_t* pmax = nullptr;      // running max of link entries per sub-segment to each (piece, peer)
     // full gossip shards: a plan per round.  Inputs every rank holds alike: the global
     // chain count cj emitted in round j (chains at most double per round), and per chunk the last
     // round's largest sub-segment count (m_out from this rank's pack, m_in from the peer's header) and
@@ -279,6 +289,7 @@ struct Handle {
     int64_t ext_lo() const { return std::max<int64_t>(0, (int64_t)lo - halo); }
     int64_t ext_hi() const { return std::min<int64_t>(g.actors, (int64_t)hi + halo); }
     uint32_t own() const { return hi - lo; }
+    int64_t piece_lo(int q, int i) const { return pbnd[(size_t)q * (npiece + 1) + i]; }
 
     Launch L() const { return Launch{grid, stream}; }
 
@@ -298,6 +309,8 @@ struct Handle {
         a.full = full ? 1u : 0u;
         a.nodes = (uint32_t)lay.nodes;
         a.span = span;
+        a.olo = lo;
+        a.ohi = hi;
         if (gossip) a.threshold = (uint32_t)cfg.gossip_threshold;
         else a.act_thr = act_thr;
         a.delta = cfg.delta;
@@ -441,13 +454,21 @@ int build_links(Handle* h) {
             HIP_TRY(hipGetLastError());
         }
     }
-    if (h->sharded) {  // link counts per (source rank, destination rank, sender degree)
-        const size_t nb = (size_t)h->world * h->world * 8;
+    if (h->sharded) {  // link counts per (source piece, destination rank, sender degree)
+        const int K = h->npiece, W = h->world;
+        const size_t nb = (size_t)W * K * W * 8;
+        HistBounds hb{};
+        hb.ns = (uint32_t)(W * K);
+        hb.nd = (uint32_t)W;
+        for (int q = 0; q < W; ++q)
+            for (int i = 0; i < K; ++i) hb.sb[q * K + i] = (uint32_t)h->piece_lo(q, i);
+        hb.sb[W * K] = (uint32_t)h->abnd[W];
+        for (int q = 0; q <= W; ++q) hb.db[q] = (uint32_t)h->abnd[q];
         unsigned long long* hist = nullptr;
         HIP_TRY(hipMalloc(&hist, nb * sizeof *hist));
         e = hipMemsetAsync(hist, 0, nb * sizeof *hist, s);
         if (e == hipSuccess) {
-            launch_link_hist(seed, h->g, base_xchg(h), hist, l);
+            launch_link_hist(seed, h->g, hb, hist, l);
             h->lhist.assign(nb, 0);
             e = hipMemcpyAsync(h->lhist.data(), hist, nb * sizeof *hist, hipMemcpyDeviceToHost, s);
         }
@@ -572,9 +593,11 @@ int reset(Handle* h) {
     h->converged = false;
     h->batch = 8;
     h->awaiting_deliver = false;
+    h->piece_next = 0;
+    h->round_slot = -1;
     h->timed_count = 0;
     if (h->sharded) {  // the full plan, no restore point
-        HIP_TRY(hipMemsetAsync(h->pmax, 0, kMaxWorld * sizeof(uint32_t), h->stream));
+        HIP_TRY(hipMemsetAsync(h->pmax, 0, (size_t)kMaxPieces * kMaxWorld * sizeof(uint32_t), h->stream));
         if (h->cparts) {  // full gossip's per-round plan inputs and done-word shipping state
             HIP_TRY(hipMemsetAsync(h->cparts, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t), h->stream));
             HIP_TRY(hipMemsetAsync(h->pstat, 0, kPstatWords * sizeof(uint32_t), h->stream));
@@ -673,10 +696,20 @@ int clear_tags_if_due(Handle* h, uint32_t r) {
 // The dominant round kernel F(k) (timed under GP_FLAG_KERNEL_TIMING) ...  A shard samples the
 // timing of every kTimeEvery-th round (`timed`), and counts the actors its quiet kernel walks in
 // exactly those rounds, so work_per_launch and avg_ms average over the same launches.
-void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed) {
+// Piece i of a shard's round: the launch walks the piece's actors on a grid for them.
+void piece_args(const Handle* h, int piece, RoundArgs& a, Launch& l) {
+    if (h->npiece <= 1) return;
+    a.lo = (uint32_t)h->piece_lo(h->rank, piece);
+    a.hi = (uint32_t)h->piece_lo(h->rank, piece + 1);
+    l.grid = grid_for(a.hi - a.lo);
+    a.span = span_for(a.hi - a.lo, l.grid);
+}
+
+void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed, int piece = 0) {
     RoundArgs a = h->args((uint32_t)k);
     if (h->sharded && !timed) a.work = nullptr;
-    const Launch l = h->L();
+    Launch l = h->L();
+    piece_args(h, piece, a, l);
     if (h->gossip) {
         if (h->generic) {  // adds into inc_cur, consumed (zeroed) by F(k+1)
             if (x) launch_gs_full4x(a, *x, l);
@@ -705,13 +738,15 @@ void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed) {
 }
 
 // ... and the passes that complete round k after it (link scatter; bucket scan + fill).
-int launch_aux(Handle* h, int64_t k, const Xchg* x) {
+int launch_aux(Handle* h, int64_t k, const Xchg* x, int piece = 0) {
     const uint32_t r = (uint32_t)k;
-    const RoundArgs a = h->args(r);
-    const Launch l = h->L();
+    RoundArgs a = h->args(r);
+    Launch l = h->L();
+    piece_args(h, piece, a, l);
     int rc;
     // (a shard clears before its round kernel: its tail rounds write their own link marks)
     if (!fused_marks(h) && !h->sharded && (rc = clear_tags_if_due(h, r))) return rc;
+    (void)rc;
     if (h->gossip) {
         if (!h->generic && h->g.has_link) {
             if (x) launch_gs_link_scatter_x(a, *x, l);
@@ -761,15 +796,18 @@ int clear_act_if_due(Handle* h, int64_t k) {
 }
 
 // Round k with its three timing events (slot i of the event ring).
-int launch_round(Handle* h, int64_t k, const Xchg* x, bool timing, int64_t i) {
+// (In pieces, the events bracket the whole round: piece 0's round kernel to the last piece's round
+// kernel, then the last piece's pass; the earlier pieces' passes count as round kernel time.)
+int launch_round(Handle* h, int64_t k, const Xchg* x, bool timing, int64_t i, int piece = 0) {
     int rc;
-    if ((fused_marks(h) || h->sharded) && (rc = clear_tags_if_due(h, (uint32_t)k))) return rc;
-    if ((rc = clear_act_if_due(h, k))) return rc;
-    if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i], h->stream));
-    launch_main(h, k, x, timing);
-    if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i + 1], h->stream));
-    if ((rc = launch_aux(h, k, x))) return rc;
-    if (timing) HIP_TRY(hipEventRecord(h->kev[3 * i + 2], h->stream));
+    const bool first = piece == 0, last = piece == h->npiece - 1;
+    if (first && (fused_marks(h) || h->sharded) && (rc = clear_tags_if_due(h, (uint32_t)k))) return rc;
+    if (first && (rc = clear_act_if_due(h, k))) return rc;
+    if (timing && first) HIP_TRY(hipEventRecord(h->kev[3 * i], h->stream));
+    launch_main(h, k, x, timing, piece);
+    if (timing && last) HIP_TRY(hipEventRecord(h->kev[3 * i + 1], h->stream));
+    if ((rc = launch_aux(h, k, x, piece))) return rc;
+    if (timing && last) HIP_TRY(hipEventRecord(h->kev[3 * i + 2], h->stream));
     return GP_OK;
 }
 
@@ -965,11 +1003,13 @@ Chunk shaped(const Chunk& full, uint32_t cap, uint32_t dpairs) {
     return c;
 }
 
-Chunk chunk_layout(const Handle* h, int p, int q) {
+// Chunk p -> q of piece i: the header; the halo face when the piece holds it (p's first plane, in its
+// first piece, to p-1; its last plane, in its last piece, to p+1); the entries of the piece's senders.
+Chunk chunk_layout(const Handle* h, int p, int q, int i) {
     Chunk c;
     size_t off = kAlign;  // ShardHeader
     const int64_t size_p = h->abnd[p + 1] - h->abnd[p];
-    if (h->halo && (q == p - 1 || q == p + 1)) {  // p's first (to p-1) or last (to p+1) actors
+    if (h->halo && ((q == p - 1 && i == 0) || (q == p + 1 && i == h->npiece - 1))) {
         c.halo = (uint32_t)std::min<int64_t>(h->halo, size_p);
         c.hdir = off;
         off = align_up(off + c.halo);
@@ -1005,7 +1045,7 @@ Chunk chunk_layout(const Handle* h, int p, int q) {
         exact = chains;  // one sub-segment's bound
     } else if (h->g.has_link) {
         for (int d = 1; d < 8; ++d) {
-            const double n = (double)h->lhist[((size_t)p * h->world + q) * 8 + d];
+            const double n = (double)h->lhist[(((size_t)p * h->npiece + i) * h->world + q) * 8 + d];
             const double pick = h->gossip ? 1.0 - (1.0 - 1.0 / d) * (1.0 - 1.0 / d) : 1.0 / d;
             mean += n * pick;
             exact += n;
@@ -1017,59 +1057,68 @@ Chunk chunk_layout(const Handle* h, int p, int q) {
     return shaped(c, c.cap, 0);
 }
 
-// The current plan: chunk p -> q of every peer with the link capacities out_cap[q] / in_cap[q]
-// (the full plan's at most) and done parts of out_dp[q] / in_dp[q] pairs (0: every word), packed
-// from offset 0 of the send / receive buffers.
+// The current plan: chunk (piece i, peer q), index c = i * world + q, with the link capacities
+// out_cap[c] / in_cap[c] (the full plan's at most) and done parts of out_dp[c] / in_dp[c] pairs (0:
+// every word), packed piece-major from offset 0 of the send / receive buffers.
 void apply_plan(Handle* h, const std::vector<uint32_t>& out_cap, const std::vector<uint32_t>& in_cap,
                 const std::vector<uint32_t>* out_dp = nullptr, const std::vector<uint32_t>* in_dp = nullptr) {
-    const int W = h->world;
+    const int W = h->world, K = h->npiece;
     int64_t so = 0, ro = 0;
-    h->max_in_cap = 0;
-    for (int q = 0; q < W; ++q) {
-        if (q != h->rank) {
-            h->out_chunk[q] = shaped(h->full_out[q], std::min(out_cap[q], h->full_out[q].cap), out_dp ? (*out_dp)[q] : 0u);
-            h->in_chunk[q] = shaped(h->full_in[q], std::min(in_cap[q], h->full_in[q].cap), in_dp ? (*in_dp)[q] : 0u);
-            h->max_in_cap = std::max(h->max_in_cap, h->in_chunk[q].cap);
+    for (int i = 0; i < K; ++i) {
+        h->out_poff[i] = so;
+        h->in_poff[i] = ro;
+        h->max_in_cap[i] = 0;
+        for (int q = 0; q < W; ++q) {
+            const size_t c = (size_t)i * W + q;
+            if (q != h->rank) {
+                h->out_chunk[c] = shaped(h->full_out[c], std::min(out_cap[c], h->full_out[c].cap), out_dp ? (*out_dp)[c] : 0u);
+                h->in_chunk[c] = shaped(h->full_in[c], std::min(in_cap[c], h->full_in[c].cap), in_dp ? (*in_dp)[c] : 0u);
+                h->max_in_cap[i] = std::max(h->max_in_cap[i], h->in_chunk[c].cap);
+            }
+            h->out_off[c] = so;
+            h->in_off[c] = ro;
+            so += (int64_t)h->out_chunk[c].size;
+            ro += (int64_t)h->in_chunk[c].size;
         }
-        h->out_off[q] = so;
-        h->in_off[q] = ro;
-        so += (int64_t)h->out_chunk[q].size;
-        ro += (int64_t)h->in_chunk[q].size;
     }
+    h->out_poff[K] = so;
+    h->in_poff[K] = ro;
 }
 
 void full_plan(Handle* h) {
-    std::vector<uint32_t> o((size_t)h->world), i((size_t)h->world);
-    for (int q = 0; q < h->world; ++q) {
-        o[q] = h->full_out[q].cap;
-        i[q] = h->full_in[q].cap;
+    const size_t n = (size_t)h->npiece * h->world;
+    std::vector<uint32_t> o(n), i(n);
+    for (size_t c = 0; c < n; ++c) {
+        o[c] = h->full_out[c].cap;
+        i[c] = h->full_in[c].cap;
     }
     apply_plan(h, o, i);
 }
 
 int build_plan(Handle* h) {
-    const int W = h->world, p = h->rank;
-    h->full_out.assign((size_t)W, Chunk{});
-    h->full_in.assign((size_t)W, Chunk{});
-    h->out_chunk.assign((size_t)W, Chunk{});
-    h->in_chunk.assign((size_t)W, Chunk{});
-    h->out_off.assign((size_t)W, 0);
-    h->in_off.assign((size_t)W, 0);
-    for (int q = 0; q < W; ++q)
-        if (q != p) {
-            h->full_out[q] = chunk_layout(h, p, q);
-            h->full_in[q] = chunk_layout(h, q, p);
-        }
+    const int W = h->world, p = h->rank, K = h->npiece;
+    const size_t n = (size_t)K * W;
+    h->full_out.assign(n, Chunk{});
+    h->full_in.assign(n, Chunk{});
+    h->out_chunk.assign(n, Chunk{});
+    h->in_chunk.assign(n, Chunk{});
+    h->out_off.assign(n, 0);
+    h->in_off.assign(n, 0);
+    h->out_poff.assign((size_t)K + 1, 0);
+    h->in_poff.assign((size_t)K + 1, 0);
+    h->max_in_cap.assign((size_t)K, 0u);
+    for (int i = 0; i < K; ++i)
+        for (int q = 0; q < W; ++q)
+            if (q != p) {
+                h->full_out[(size_t)i * W + q] = chunk_layout(h, p, q, i);
+                h->full_in[(size_t)i * W + q] = chunk_layout(h, q, p, i);
+            }
     full_plan(h);
-    h->send_total = 0;
-    h->recv_total = 0;
-    for (int q = 0; q < W; ++q) {
-        h->send_total += (int64_t)h->out_chunk[q].size;
-        h->recv_total += (int64_t)h->in_chunk[q].size;
-    }
+    h->send_total = h->out_poff[K];
+    h->recv_total = h->in_poff[K];
     int rc;
     if ((rc = h->alloc(&h->pcount, ((size_t)W + 2) * kSub * kCtrStride)) || (rc = h->alloc(&h->overflow, 1)) ||
-        (rc = h->alloc(&h->self_newly, 1)) || (rc = h->alloc(&h->pmax, kMaxWorld)))
+        (rc = h->alloc(&h->self_newly, 1)) || (rc = h->alloc(&h->pmax, (size_t)kMaxPieces * kMaxWorld)))
         return rc;
     return GP_OK;
 }
@@ -1095,20 +1144,24 @@ Xchg base_xchg(const Handle* h) {
     return x;
 }
 
-Xchg make_xchg(const Handle* h, void* send, const void* recv) {
+// The exchange descriptor of piece i (the round's only piece unless it runs in pieces).
+Xchg make_xchg(const Handle* h, void* send, const void* recv, int i = 0) {
     Xchg x = base_xchg(h);
+    const int W = h->world;
+    x.last = i == h->npiece - 1 ? 1u : 0u;
+    x.pmax = h->pmax + (size_t)i * kMaxWorld;
     for (int q = 0; q < h->world; ++q) {
         if (q == h->rank) continue;
         if (send) {
-            char* b = static_cast<char*>(send) + h->out_off[q];
-            const Chunk& c = h->out_chunk[q];
+            char* b = static_cast<char*>(send) + h->out_off[(size_t)i * W + q];
+            const Chunk& c = h->out_chunk[(size_t)i * W + q];
             x.out[q] = PeerOut{reinterpret_cast<ShardHeader*>(b), reinterpret_cast<uint32_t*>(b + c.slot),
                                c.msg ? reinterpret_cast<double2*>(b + c.msg) : nullptr, c.cap, c.dpairs,
                                c.done ? reinterpret_cast<uint32_t*>(b + c.done) : nullptr};
         }
         if (recv) {
-            const char* b = static_cast<const char*>(recv) + h->in_off[q];
-            const Chunk& c = h->in_chunk[q];
+            const char* b = static_cast<const char*>(recv) + h->in_off[(size_t)i * W + q];
+            const Chunk& c = h->in_chunk[(size_t)i * W + q];
             x.in[q] = PeerIn{reinterpret_cast<const ShardHeader*>(b), reinterpret_cast<const uint32_t*>(b + c.slot),
                              c.msg ? reinterpret_cast<const double2*>(b + c.msg) : nullptr, c.cap, c.dpairs,
                              c.done ? reinterpret_cast<const uint32_t*>(b + c.done) : nullptr};
@@ -1120,9 +1173,10 @@ Xchg make_xchg(const Handle* h, void* send, const void* recv) {
         const int q = side ? p + 1 : p - 1;
         if (q < 0 || q >= h->world) continue;
         x.h.code[side] = h->g.gz > 1 ? (side ? 5u : 4u) : (side ? 1u : 0u);
-        const Chunk& co = h->out_chunk[q];
+        const size_t c = (size_t)i * W + q;  // (a face travels in one piece only: chunk_layout)
+        const Chunk& co = h->out_chunk[c];
         if (send && co.halo) {
-            char* b = static_cast<char*>(send) + h->out_off[q];
+            char* b = static_cast<char*>(send) + h->out_off[c];
             x.h.out_n[side] = co.halo;
             x.h.out_first[side] = side ? h->hi - co.halo : h->lo;
             x.h.out_cap[side] = co.hcap;
@@ -1132,9 +1186,9 @@ Xchg make_xchg(const Handle* h, void* send, const void* recv) {
                 x.h.out_msg[side] = reinterpret_cast<double2*>(b + co.hmsg);
             }
         }
-        const Chunk& ci = h->in_chunk[q];
+        const Chunk& ci = h->in_chunk[c];
         if (recv && ci.halo) {
-            const char* b = static_cast<const char*>(recv) + h->in_off[q];
+            const char* b = static_cast<const char*>(recv) + h->in_off[c];
             x.h.in_n[side] = ci.halo;
             x.h.in_first[side] = side ? h->hi : h->lo - ci.halo;
             x.h.in_cap[side] = ci.hcap;
@@ -1152,33 +1206,51 @@ Xchg make_xchg(const Handle* h, void* send, const void* recv) {
 // Index of the round F(k) applies (its completion count), -1 for gossip's emit-only F(0).
 long long applied_round(const Handle* h, int64_t k) { return h->gossip ? (long long)k - 1 : (long long)k; }
 
-int shard_round(Handle* h, void* send) {
+// Piece `piece` of round k: its round kernel and link pass, the halo face it holds, its headers.  The
+// pieces of a round are packed in order; the last one completes the round (gp_shard_deliver next).
+int shard_round_piece(Handle* h, void* send, int piece) {
     if (h->awaiting_deliver) return fail(GP_ESTATE, "gp_shard_deliver must follow gp_shard_round");
+    if (piece != h->piece_next)
+        return fail(GP_ESTATE, "piece %d packed out of order (next: %d of %d)", piece, h->piece_next, h->npiece);
     if (!send && h->send_total) return fail(GP_EINVAL, "null send buffer");
     if (reinterpret_cast<uintptr_t>(send) % kAlign) return fail(GP_EINVAL, "send buffer not %zu-byte aligned", kAlign);
     const bool timing = (h->cfg.flags & GP_FLAG_KERNEL_TIMING) != 0;
     const int64_t k = h->next_kernel;
     int rc;
-    if ((rc = ensure_trace(h, k + 4))) return rc;
-    const Xchg x = make_xchg(h, send, nullptr);
-    // kernel timing samples every kTimeEvery-th round (event records cost stream time)
-    if (timing && k >= (h->gossip ? 1 : 0) && k % kTimeEvery == 0) {
-        if ((rc = ensure_events(h, h->timed_count + 1))) return rc;
-        h->timed_round.resize((size_t)h->timed_count + 1);
-        h->timed_round[(size_t)h->timed_count] = applied_round(h, k);
-        if ((rc = launch_round(h, k, &x, true, h->timed_count))) return rc;
-        ++h->timed_count;
-    } else if ((rc = launch_round(h, k, &x, false, 0))) {
-        return rc;
+    if (piece == 0) {
+        if ((rc = ensure_trace(h, k + 4))) return rc;
+        // kernel timing samples every kTimeEvery-th round (event records cost stream time)
+        h->round_slot = -1;
+        if (timing && k >= (h->gossip ? 1 : 0) && k % kTimeEvery == 0) {
+            if ((rc = ensure_events(h, h->timed_count + 1))) return rc;
+            h->timed_round.resize((size_t)h->timed_count + 1);
+            h->timed_round[(size_t)h->timed_count] = applied_round(h, k);
+            h->round_slot = h->timed_count++;
+        }
     }
+    const Xchg x = make_xchg(h, send, nullptr, piece);
+    if ((rc = launch_round(h, k, &x, h->round_slot >= 0, std::max<int64_t>(h->round_slot, 0), piece))) return rc;
     const RoundArgs a = h->args((uint32_t)k);
-    // halo faces (this rank's first actors to rank-1, its last actors to rank+1), then the headers
+    // the halo face this piece holds (the rank's first actors to rank-1, its last to rank+1), then the
+    // headers
     launch_shard_halo(a, x, h->gossip ? 0 : 1, h->stream);
     launch_shard_pack(a, x, applied_round(h, k), h->stream);
     HIP_TRY(hipGetLastError());
-    h->awaiting_deliver = true;
-    h->pending_send = send;
-    for (int q = 0; q < h->world; ++q) h->bytes_sent += (int64_t)h->out_chunk[q].size;
+    for (int q = 0; q < h->world; ++q) h->bytes_sent += (int64_t)h->out_chunk[(size_t)piece * h->world + q].size;
+    if (++h->piece_next == h->npiece) {
+        h->piece_next = 0;
+        h->awaiting_deliver = true;
+        h->pending_send = send;
+    }
+    return GP_OK;
+}
+
+int shard_round(Handle* h, void* send) {
+    if (h->piece_next) return fail(GP_ESTATE, "gp_shard_round in the middle of a round's pieces");
+    for (int i = 0; i < h->npiece; ++i) {
+        const int rc = shard_round_piece(h, send, i);
+        if (rc) return rc;
+    }
     return GP_OK;
 }
 
@@ -1187,16 +1259,19 @@ int shard_deliver(Handle* h, const void* recv) {
     if (!recv && h->recv_total) return fail(GP_EINVAL, "null receive buffer");
     if (reinterpret_cast<uintptr_t>(recv) % kAlign) return fail(GP_EINVAL, "receive buffer not %zu-byte aligned", kAlign);
     const int64_t k = h->next_kernel;
-    // the halo faces (rank-1's last actors land below lo, rank+1's first at hi) and the link
-    // entries are applied by one kernel
-    const Xchg x = make_xchg(h, h->pending_send, recv);
-    // the grid covers the largest per-peer part: link entries, a halo face, or (full gossip) a
-    // peer's done-bitmap words, which arrive whole whatever the plan
-    uint32_t most = std::max(kSub * h->max_in_cap, h->halo);
-    if (h->gossip && h->full)
-        for (int q = 0; q < h->world; ++q) most = std::max(most, (uint32_t)((h->abnd[q + 1] - h->abnd[q]) / 32 + 2));
-    launch_shard_unpack(h->args((uint32_t)k), x, applied_round(h, k), most, h->gossip ? 1 : 0, h->full ? 1 : 0,
-                        h->stream);
+    // one kernel per piece applies its halo face (rank-1's last actors land below lo, rank+1's first
+    // at hi) and link entries; the last publishes the round's count
+    for (int i = 0; i < h->npiece; ++i) {
+        const Xchg x = make_xchg(h, h->pending_send, recv, i);
+        // the grid covers the largest per-peer part: link entries, a halo face, or (full gossip) a
+        // peer's done-bitmap words, which arrive whole whatever the plan
+        const bool face = i == 0 || i == h->npiece - 1;  // (the halo faces travel in the end pieces)
+        uint32_t most = std::max(kSub * h->max_in_cap[i], face ? h->halo : 0u);
+        if (h->gossip && h->full)
+            for (int q = 0; q < h->world; ++q) most = std::max(most, (uint32_t)((h->abnd[q + 1] - h->abnd[q]) / 32 + 2));
+        launch_shard_unpack(h->args((uint32_t)k), x, applied_round(h, k), most, h->gossip ? 1 : 0, h->full ? 1 : 0,
+                            h->stream);
+    }
     HIP_TRY(hipGetLastError());
     h->awaiting_deliver = false;
     h->last_recv = recv;
@@ -1389,7 +1464,7 @@ int restore(Handle* h, int64_t reached) {
     if (h->cparts) HIP_TRY(hipMemsetAsync(h->cparts, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(h->pcount, 0, ((size_t)h->world + 2) * kSub * kCtrStride * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(h->overflow, 0, sizeof(uint32_t), s));
-    HIP_TRY(hipMemsetAsync(h->pmax, 0, kMaxWorld * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(h->pmax, 0, (size_t)kMaxPieces * kMaxWorld * sizeof(uint32_t), s));
     HIP_TRY(hipStreamSynchronize(s));
     if (gossip_plans(h)) {  // the chain count of the restore point; no round seen since
         h->gpl.j = c.gj;
@@ -1419,23 +1494,29 @@ int choose_plan(Handle* h) {
     // rank's were reset, the peers' last headers were not)
     if (!h->delivered) return GP_OK;
     h->delivered = 0;
-    const int W = h->world;
+    const int W = h->world, K = h->npiece;
+    const size_t n = (size_t)K * W;
     const bool tight = (h->cfg.flags & GP_FLAG_TIGHT_TIERS) != 0;
-    std::vector<uint32_t> mo((size_t)kMaxWorld, 0u), mi((size_t)W, 0u);
-    HIP_TRY(hipMemcpy(mo.data(), h->pmax, kMaxWorld * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    for (int q = 0; q < W && h->last_recv; ++q)
-        if (q != h->rank)
-            HIP_TRY(hipMemcpy(&mi[q], static_cast<const char*>(h->last_recv) + h->in_off[q] + offsetof(ShardHeader, runmax),
-                              sizeof(uint32_t), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemsetAsync(h->pmax, 0, kMaxWorld * sizeof(uint32_t), h->stream));
+    // per (piece, peer): this rank's running maxima, and the peers' from the headers they sent last
+    std::vector<uint32_t> pm((size_t)kMaxPieces * kMaxWorld, 0u), mo(n, 0u), mi(n, 0u);
+    HIP_TRY(hipMemcpy(pm.data(), h->pmax, pm.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (int i = 0; i < K; ++i)
+        for (int q = 0; q < W; ++q) {
+            const size_t c = (size_t)i * W + q;
+            mo[c] = pm[(size_t)i * kMaxWorld + q];
+            if (q != h->rank && h->last_recv)
+                HIP_TRY(hipMemcpy(&mi[c], static_cast<const char*>(h->last_recv) + h->in_off[c] + offsetof(ShardHeader, runmax),
+                                  sizeof(uint32_t), hipMemcpyDeviceToHost));
+        }
+    HIP_TRY(hipMemsetAsync(h->pmax, 0, (size_t)kMaxPieces * kMaxWorld * sizeof(uint32_t), h->stream));
     // global conditions only (every rank decides alike): half the nodes converged (the tail), no
     // replay in progress, a batch already run
     const bool on = !h->converged && h->last_recv && h->rounds >= h->full_until &&
                     (tight || h->completed * 2 >= h->lay.nodes);
-    std::vector<uint32_t> oc((size_t)W), ic((size_t)W);
-    for (int q = 0; q < W; ++q) {
-        oc[q] = on ? tier_cap(h->full_out[q].cap, mo[q], tight) : h->full_out[q].cap;
-        ic[q] = on ? tier_cap(h->full_in[q].cap, mi[q], tight) : h->full_in[q].cap;
+    std::vector<uint32_t> oc(n), ic(n);
+    for (size_t c = 0; c < n; ++c) {
+        oc[c] = on ? tier_cap(h->full_out[c].cap, mo[c], tight) : h->full_out[c].cap;
+        ic[c] = on ? tier_cap(h->full_in[c].cap, mi[c], tight) : h->full_in[c].cap;
     }
     int rc;
     if (on && (!h->ck.valid || tight || h->rounds - h->ck.rounds >= kCkptEvery)) {
@@ -1443,7 +1524,7 @@ int choose_plan(Handle* h) {
     }
     h->tiered = on;
     bool changed = false;
-    for (int q = 0; q < W; ++q) changed |= oc[q] != h->out_chunk[q].cap || ic[q] != h->in_chunk[q].cap;
+    for (size_t c = 0; c < n; ++c) changed |= oc[c] != h->out_chunk[c].cap || ic[c] != h->in_chunk[c].cap;
     if (changed) {
         apply_plan(h, oc, ic);
         ++h->plan_changes;
@@ -1614,6 +1695,26 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
     g.dx = make_fastdiv(g.gx);
     g.dy = make_fastdiv(g.gy);
     if (h->world > 1 && !h->full) h->halo = g.gz > 1 ? g.plane : 1u;  // grid rows crossing a shard face
+    // A round in pieces: push-sum pull shards whose host exchanges piece by piece
+    // (GP_FLAG_PIECES), from 2^20 actors on every rank (GP_FLAG_FORCE_PIECES: any size), in whole
+    // z-planes (line / 2D: 256 actors), so that the faces stay in the first and the last piece.
+    // The same decision on every rank: it depends on the partition only.
+    if (sharded && h->world > 1 && !h->gossip && !h->generic && (cfg->flags & GP_FLAG_PIECES)) {
+        const int64_t unit = g.gz > 1 ? (int64_t)g.plane : 256;
+        int64_t least = INT64_MAX, units = INT64_MAX;
+        for (int q = 0; q < h->world; ++q) {
+            least = std::min(least, bounds[q + 1] - bounds[q]);
+            units = std::min(units, (bounds[q + 1] - bounds[q]) / unit);
+        }
+        const bool big = least >= kPieceMinActors || (cfg->flags & GP_FLAG_FORCE_PIECES);
+        h->npiece = big && units >= kMaxPieces ? kMaxPieces : 1;
+    }
+    h->pbnd.assign((size_t)h->world * (h->npiece + 1), 0);
+    for (int q = 0; q < h->world; ++q) {
+        const int64_t unit = g.gz > 1 ? (int64_t)g.plane : 256, n = (bounds[q + 1] - bounds[q]) / unit;
+        for (int i = 0; i <= h->npiece; ++i)
+            h->pbnd[(size_t)q * (h->npiece + 1) + i] = i == h->npiece ? bounds[q + 1] : bounds[q] + n * i / h->npiece * unit;
+    }
     // leader = Random().Next(0, nodes)  (program.fs:173/211/250/316)
     h->lay.leader = scale_draw(philox(0u, 0u, kStreamLeader, cfg->seed).x, (uint32_t)nodes);
     // actors with at least one neighbour: every actor of line / 2D / full (nodes + 1 >= 2),
@@ -1817,6 +1918,11 @@ struct Group {
     std::vector<void*> send, recv;
     std::vector<ncclComm_t> comm;
     hipStream_t shared = nullptr;
+    // rounds in pieces: the exchange of each piece runs on a stream of its own per
+    // shard (xstream; one stream for the one-device copies), ordered after the piece's kernels by an
+    // event, and the shards' unpacks wait for the last one
+    std::vector<hipStream_t> xstream;
+    std::vector<hipEvent_t> ev_done, ev_x;
     int64_t batch = 8;
     int64_t rounds = 0, completed = 0;
     bool converged = false;
@@ -1825,6 +1931,13 @@ struct Group {
         for (size_t p = 0; p < shard.size(); ++p) {
             if (!one_device) (void)hipSetDevice(dev[p]);
             if (shard[p]) (void)hipStreamSynchronize(shard[p]->stream);
+            if (p < xstream.size() && xstream[p]) (void)hipStreamSynchronize(xstream[p]);
+        }
+        for (size_t p = 0; p < xstream.size(); ++p) {
+            if (!one_device) (void)hipSetDevice(dev[p]);
+            if (xstream[p]) (void)hipStreamDestroy(xstream[p]);
+            if (p < ev_done.size() && ev_done[p]) (void)hipEventDestroy(ev_done[p]);
+            if (p < ev_x.size() && ev_x[p]) (void)hipEventDestroy(ev_x[p]);
         }
         for (ncclComm_t c : comm)
             if (c) (void)rccl()->comm_destroy(c);  // a communicator exists only if RCCL loaded
@@ -1846,39 +1959,64 @@ struct Group {
 
 // Send / receive pairs of every (p, q) between ncclGroupStart and ncclGroupEnd.  An error inside
 // the group still closes it (the group is left open otherwise, and the next RCCL call fails).
-int group_exchange_rccl(Group& G, const Rccl& R) {
+// The chunks of piece i (the whole round when it is not in pieces), on stream s(p) of each shard.
+int group_exchange_rccl(Group& G, const Rccl& R, int i, bool split) {
     const int W = G.W;
     for (int p = 0; p < W; ++p) {
         const Handle* s = G.shard[p];
+        hipStream_t st = split ? G.xstream[p] : s->stream;
         for (int q = 0; q < W; ++q) {
             if (q == p) continue;
-            const size_t ns = s->out_chunk[q].size, nr = s->in_chunk[q].size;
-            if (ns) RCCL_TRY(R.send(static_cast<char*>(G.send[p]) + s->out_off[q], ns, ncclUint8, q, G.comm[p], s->stream));
-            if (nr) RCCL_TRY(R.recv(static_cast<char*>(G.recv[p]) + s->in_off[q], nr, ncclUint8, q, G.comm[p], s->stream));
+            const size_t c = (size_t)i * W + q, ns = s->out_chunk[c].size, nr = s->in_chunk[c].size;
+            if (ns) RCCL_TRY(R.send(static_cast<char*>(G.send[p]) + s->out_off[c], ns, ncclUint8, q, G.comm[p], st));
+            if (nr) RCCL_TRY(R.recv(static_cast<char*>(G.recv[p]) + s->in_off[c], nr, ncclUint8, q, G.comm[p], st));
         }
     }
     return GP_OK;
 }
 
-int group_exchange(Group& G) {
+// Piece i's exchange.  In pieces it runs on the exchange streams, after the piece's kernels (an event
+// on each shard's stream), so the shards go on with piece i+1 meanwhile.
+int group_exchange(Group& G, int i = 0) {
     const int W = G.W;
+    const bool split = G.shard[0]->npiece > 1;
+    if (split) {
+        for (int p = 0; p < (G.one_device ? 1 : W); ++p) {
+            if (!G.one_device) HIP_TRY(hipSetDevice(G.dev[p]));
+            HIP_TRY(hipEventRecord(G.ev_done[p], G.shard[p]->stream));
+            HIP_TRY(hipStreamWaitEvent(G.xstream[p], G.ev_done[p], 0));
+        }
+    }
     if (G.one_device) {
+        hipStream_t st = split ? G.xstream[0] : G.shared;
         for (int p = 0; p < W; ++p)
             for (int q = 0; q < W; ++q) {
-                const int64_t n = (int64_t)G.shard[p]->out_chunk[q].size;
+                const size_t c = (size_t)i * W + q;
+                const int64_t n = (int64_t)G.shard[p]->out_chunk[c].size;
                 if (q == p || !n) continue;
-                HIP_TRY(hipMemcpyAsync(static_cast<char*>(G.recv[q]) + G.shard[q]->in_off[p],
-                                       static_cast<char*>(G.send[p]) + G.shard[p]->out_off[q], (size_t)n,
-                                       hipMemcpyDeviceToDevice, G.shared));
+                HIP_TRY(hipMemcpyAsync(static_cast<char*>(G.recv[q]) + G.shard[q]->in_off[(size_t)i * W + p],
+                                       static_cast<char*>(G.send[p]) + G.shard[p]->out_off[c], (size_t)n,
+                                       hipMemcpyDeviceToDevice, st));
             }
         return GP_OK;
     }
     const Rccl& R = *rccl();  // loaded: the group has communicators
     RCCL_TRY(R.group_start());
-    const int rc = group_exchange_rccl(G, R);
+    const int rc = group_exchange_rccl(G, R, i, split);
     const ncclResult_t end = R.group_end();
     if (rc) return rc;
     if (end != ncclSuccess) return fail(GP_ERCCL, "ncclGroupEnd failed: %s", R.error_string(end));
+    return GP_OK;
+}
+
+// In pieces: the shards' unpacks wait for the last piece's exchange.
+int group_exchange_join(Group& G) {
+    if (G.shard[0]->npiece <= 1) return GP_OK;
+    for (int p = 0; p < (G.one_device ? 1 : G.W); ++p) {
+        if (!G.one_device) HIP_TRY(hipSetDevice(G.dev[p]));
+        HIP_TRY(hipEventRecord(G.ev_x[p], G.xstream[p]));
+        HIP_TRY(hipStreamWaitEvent(G.one_device ? G.shared : G.shard[p]->stream, G.ev_x[p], 0));
+    }
     return GP_OK;
 }
 
@@ -1912,11 +2050,15 @@ int group_step(Handle* h, int64_t max_rounds, gp_status* st) {
     while (!G.converged && G.rounds < goal) {
         const int64_t B = std::min<int64_t>(G.batch, goal - G.rounds);
         for (int64_t i = 0; i < B; ++i) {
-            for (int p = 0; p < G.W; ++p) {
-                if (!G.one_device) HIP_TRY(hipSetDevice(G.dev[p]));
-                if ((rc = shard_round(G.shard[p], G.send[p]))) return rc;
+            // piece by piece: every shard's piece j, then its exchange, which overlaps piece j+1
+            for (int j = 0; j < G.shard[0]->npiece; ++j) {
+                for (int p = 0; p < G.W; ++p) {
+                    if (!G.one_device) HIP_TRY(hipSetDevice(G.dev[p]));
+                    if ((rc = shard_round_piece(G.shard[p], G.send[p], j))) return rc;
+                }
+                if ((rc = group_exchange(G, j))) return rc;
             }
-            if ((rc = group_exchange(G))) return rc;
+            if ((rc = group_exchange_join(G))) return rc;
             for (int p = 0; p < G.W; ++p) {
                 if (!G.one_device) HIP_TRY(hipSetDevice(G.dev[p]));
                 if ((rc = shard_deliver(G.shard[p], G.recv[p]))) return rc;
@@ -2008,6 +2150,7 @@ int group_create(const gp_config* cfg, gp_layout* out, void** handle) {
         c.device = G.dev[p];
         c.num_gpus = 0;
         c.flags &= ~(GP_FLAG_ONE_DEVICE | GP_FLAG_GROUP | GP_FLAG_USE_STREAM);
+        c.flags |= GP_FLAG_PIECES;  // the group exchanges piece by piece (its own transport)
         c.stream = nullptr;
         if (G.one_device) {
             c.flags |= GP_FLAG_USE_STREAM;
@@ -2025,6 +2168,18 @@ int group_create(const gp_config* cfg, gp_layout* out, void** handle) {
             return bail(fail(GP_ENOMEM, "exchange receive buffer of %lld bytes", (long long)s->recv_total));
         bytes += lay.device_bytes + s->send_total + s->recv_total;
         if (p == 0) h->lay = lay;
+    }
+    if (G.shard[0]->npiece > 1) {  // the exchange streams and events of the pieces
+        G.xstream.assign((size_t)W, nullptr);
+        G.ev_done.assign((size_t)W, nullptr);
+        G.ev_x.assign((size_t)W, nullptr);
+        for (int p = 0; p < (G.one_device ? 1 : W); ++p) {
+            if ((rc = set_dev(G.dev[p]))) return bail(rc);
+            if (hipStreamCreateWithFlags(&G.xstream[p], hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&G.ev_done[p], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&G.ev_x[p], hipEventDisableTiming) != hipSuccess)
+                return bail(fail(GP_EHIP, "exchange stream / events of device %d", G.dev[p]));
+        }
     }
     if (!G.one_device) {
         G.comm.assign((size_t)W, nullptr);
@@ -2087,10 +2242,38 @@ int gp_partition(int64_t n_arg, int32_t topology, int32_t world, int64_t* bounds
     return GP_OK;
 }
 
+int gp_shard_pieces(void* handle) {
+    if (!handle) return fail(GP_EINVAL, "null handle");
+    Handle* h = H(handle);
+    if (!h->sharded) return fail(GP_ESTATE, "not a shard handle");
+    return h->npiece;
+}
+
+int gp_shard_plan_piece(void* handle, int32_t piece, int64_t* send_bytes, int64_t* recv_bytes, int64_t* offsets) {
+    if (!handle || !send_bytes || !recv_bytes || !offsets) return fail(GP_EINVAL, "null argument");
+    Handle* h = H(handle);
+    if (!h->sharded) return fail(GP_ESTATE, "not a shard handle");
+    if (piece < 0 || piece >= h->npiece) return fail(GP_EINVAL, "piece %d outside 0..%d", piece, h->npiece - 1);
+    for (int q = 0; q < h->world; ++q) {
+        send_bytes[q] = (int64_t)h->out_chunk[(size_t)piece * h->world + q].size;
+        recv_bytes[q] = (int64_t)h->in_chunk[(size_t)piece * h->world + q].size;
+    }
+    offsets[0] = h->out_poff[piece];
+    offsets[1] = h->in_poff[piece];
+    return GP_OK;
+}
+
+int gp_shard_round_piece(void* handle, void* send_buf, int32_t piece) {
+    if (!handle) return fail(GP_EINVAL, "null handle");
+    if (!H(handle)->sharded) return fail(GP_ESTATE, "not a shard handle");
+    return shard_round_piece(H(handle), send_buf, piece);
+}
+
 int gp_shard_plan(void* handle, int64_t* send_bytes, int64_t* recv_bytes) {
     if (!handle || !send_bytes || !recv_bytes) return fail(GP_EINVAL, "null argument");
     Handle* h = H(handle);
     if (!h->sharded) return fail(GP_ESTATE, "not a shard handle");
+    if (h->npiece > 1) return fail(GP_ESTATE, "the round runs in %d pieces: gp_shard_plan_piece", h->npiece);
     for (int q = 0; q < h->world; ++q) {
         send_bytes[q] = (int64_t)h->out_chunk[q].size;
         recv_bytes[q] = (int64_t)h->in_chunk[q].size;
@@ -2324,12 +2507,8 @@ int gp_shard_stats(void* handle, gp_shard_counters* out) {
     std::memset(out, 0, sizeof *out);
     out->plan_changes = h->plan_changes;
     out->restores = h->restores;
-    out->send_bytes = 0;
-    out->recv_bytes = 0;
-    for (int q = 0; q < h->world; ++q) {
-        out->send_bytes += (int64_t)h->out_chunk[q].size;
-        out->recv_bytes += (int64_t)h->in_chunk[q].size;
-    }
+    out->send_bytes = h->out_poff[h->npiece];
+    out->recv_bytes = h->in_poff[h->npiece];
     out->restore_round = h->ck.valid ? h->ck.rounds : -1;
     out->bytes_sent = h->bytes_sent;
     return GP_OK;

@@ -20,6 +20,7 @@ constexpr int kPartStride = 16;     // u32 words between sub-counters
 constexpr int kPartRing = 4;        // rounds kept in the sub-counter ring
 constexpr int kWorkStride = 8;      // u64 words between the walked-actor sub-counters
 constexpr int kMaxWorld = 16;
+constexpr int kMaxPieces = 4;       // a shard's round in at most this many pieces
 // Exchange entries to one peer are appended into kSub sub-segments (sub = blockIdx % kSub), each
 // with its own counter on its own 128 B line: same-address atomics serialise in L2 (measured at
 // 8 loopback shards: one counter per peer cost 8.5 ms per round).
@@ -54,7 +55,8 @@ __host__ __device__ inline bool tag_clear_round(uint32_t r) { return r >= 2u && 
 struct RoundArgs {
     Geom g;
     uint64_t seed;
-    uint32_t lo, hi;       // actors this kernel updates: [0, actors), or a shard's node range
+    uint32_t lo, hi;       // actors this kernel updates: [0, actors), a shard's node range, or one piece
+                           // of it when a shard's round runs in pieces
     uint32_t tag_prev;     // link_tag(r - 1): marks of the messages collected by F(r)
     uint32_t tag_cur;      // link_tag(r): marks written for the messages F(r) emits
     uint32_t slot_lo;      // first link slot held here (0, or the shard's first): the in-bounds
@@ -65,6 +67,9 @@ struct RoundArgs {
     uint32_t full;         // full topology (implicit k + (k >= v) neighbour map)
     uint32_t nodes;        // `nodes` (full topology degree)
     uint32_t span;         // per-XCD contiguous node range (XCD-aware block mapping)
+    // The rank's own actors [olo, ohi) (= [lo, hi) unless the launch walks one piece): which sources
+    // are remote, which targets a shard marks itself.
+    uint32_t olo, ohi;
     union {  // gossip | push-sum (a handle runs one algorithm; the kernel arguments stay small)
         uint32_t threshold;  // gossip report threshold (program.fs:102)
         uint32_t act_thr;    // quiet-wave marks kept from this many converged actors (below)
@@ -187,6 +192,8 @@ struct HaloX {
 
 struct Xchg {
     uint32_t world, rank;
+    uint32_t last;                 // the round's last piece: its headers carry the
+                                   // round's count (pack), its unpack publishes total[applied]
     uint32_t abnd[kMaxWorld + 1];  // actor range of every rank
     uint32_t sbnd[kMaxWorld + 1];  // link-slot range of every rank (global CSR numbering)
     uint32_t* pcount;              // entry counters of the current round, (peer, sub) then (world +
@@ -283,8 +290,13 @@ void launch_shard_pack(const RoundArgs& a, const Xchg& x, long long applied, hip
 // entries into msg_cur + lcnt_cur / lcnt_cur / inc_cur
 void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, uint32_t max_cap, int gossip,
                          int full, hipStream_t s);
-// per-(source rank, destination rank, degree) counts of extra links, for the exchange plan
-void launch_link_hist(uint64_t seed, const Geom& g, const Xchg& x, unsigned long long* hist, const Launch& l);
+// per-(source piece, destination rank, degree) counts of extra links, for the exchange plan: sb[0..ns]
+// the source pieces' actor bounds (every rank's pieces in order), db[0..nd] the ranks'
+struct HistBounds {
+    uint32_t sb[kMaxWorld * kMaxPieces + 1], db[kMaxWorld + 1];
+    uint32_t ns, nd;
+};
+void launch_link_hist(uint64_t seed, const Geom& g, const HistBounds& b, unsigned long long* hist, const Launch& l);
 
 // setup / utility kernels
 // extra-link CSR construction (links recomputed by link_of)

@@ -496,7 +496,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) rest |= lk[k] ? 1u << k : 0u;
                 auto msg_of = [&](uint32_t k, uint32_t u) -> const double2* {
-                    if (LM == 2 && (u < a.lo || u >= a.hi)) return a.rmsg_prev + (li + k);
+                    if (LM == 2 && (u < a.olo || u >= a.ohi)) return a.rmsg_prev + (li + k);
                     return a.msg_prev + u;
                 };
                 uint32_t fs[kFiredLoads];
@@ -510,7 +510,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
 #pragma unroll
                     for (uint32_t q = 1; q < kLinkUnroll; ++q) u = k == q ? ls[q] : u;
                     fs[j] = u;
-                    fm[j] = *(fv[j] ? msg_of(k, u) : a.msg_prev + (a.lo));
+                    fm[j] = *(fv[j] ? msg_of(k, u) : a.msg_prev + a.lo);
                     rest &= rest - 1u;
                 }
 #pragma unroll
@@ -534,7 +534,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                     if constexpr (LM == 3) {  // the slot holds the message: its address needs only li,
                                               // so the load goes out with the sources and marks
                         lm[k] = load_sel(a.rmsg_prev, k < nl, li + k, a.slot_lo);
-                    } else if (LM == 2 && lk[k] && (ls[k] < a.lo || ls[k] >= a.hi)) {
+                    } else if (LM == 2 && lk[k] && (ls[k] < a.olo || ls[k] >= a.ohi)) {
                         lm[k] = a.rmsg_prev[li + k];
                     } else {
                         lm[k] = load_sel(a.msg_prev, lk[k], ls[k], a.lo);
@@ -551,7 +551,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                 if (a.lcnt_prev[li + k] == a.tag_prev) {
                     const uint32_t u = a.rev_src[li + k];
                     flush(u);
-                    add(LM == 3 || (LM == 2 && (u < a.lo || u >= a.hi)) ? a.rmsg_prev[li + k] : a.msg_prev[u]);
+                    add(LM == 3 || (LM == 2 && (u < a.olo || u >= a.ohi)) ? a.rmsg_prev[li + k] : a.msg_prev[u]);
                 }
             }
         }
@@ -590,7 +590,9 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
             const uint32_t tv = dir_target(g, v, code, code == kDirLink ? link_of(a.seed, v, a.nodes) : 0u);
             // a shard marks its own actors only: the receiver of a message that leaves the range
             // marks it when the exchange delivers it (k_shard_unpack)
-            if (!a.sharded || tv - a.lo < a.hi - a.lo) byte_store<GP_ACT_POL>(&a.act_cur[tv >> kActShift], t);
+            // (LM 1 and 3 run on one GPU only)
+            if (LM == 1 || LM == 3 || !a.sharded || tv - a.olo < a.ohi - a.olo)
+                byte_store<GP_ACT_POL>(&a.act_cur[tv >> kActShift], t);
         }
     }
     return o.conv_now ? 1u : 0u;
@@ -633,7 +635,8 @@ __device__ __forceinline__ TailWalk tail_walk(const RoundArgs& a, bool tail) {
     __shared__ uint32_t seg_list[kBlock / 64u * kTailList];
     TailWalk t;
     // segments are global (actor >> kActShift): a shard walks the ones that hold its actors
-    // [lo, hi); a segment astride lo or hi is walked by both ranks, each for its own actors
+    // [lo, hi) (its piece's); a segment astride lo or hi is walked by both ranks, each for its own
+    // actors (piece bounds inside a rank's range are whole segments)
     const uint32_t sg0 = a.lo >> kActShift, sg1 = (a.hi + kActSeg - 1u) >> kActShift, nseg = sg1 - sg0;
     const uint32_t grp = blockIdx.x & 7u, wpg = (gridDim.x >> 3) * (kBlock / 64u);
     const uint32_t wid = (blockIdx.x >> 3) * (kBlock / 64u) + (threadIdx.x >> 6);
@@ -1124,8 +1127,10 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(RoundArgs a, Xchg x, long
             chains += __shfl_xor(chains, off, 64);
         }
         if (threadIdx.x == 0) {
-            *x.self_newly = newly;
-            newly_s = newly;
+            // the round's count travels with its last piece (the round kernel's pieces all add into
+            // the same sub-counters)
+            if (x.last) *x.self_newly = newly;
+            newly_s = x.last ? newly : 0ull;
             chains_s = chains;
             if (x.self_chains) *x.self_chains = chains;
             dirty_s = 0u;
@@ -1230,7 +1235,8 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
                 t += x.in[q].hdr->newly;
                 of |= x.in[q].hdr->overflow;
             }
-        a.total[applied] = (applied >= 1 ? a.total[applied - 1] : 0ull) + t;
+        // every piece's headers carry the senders' overflow flags; the last one the round's counts
+        if (x.last) a.total[applied] = (applied >= 1 ? a.total[applied - 1] : 0ull) + t;
         if (of) atomicOr(x.overflow, 1u);
     }
     if (x.pstat && blockIdx.x == 0 && threadIdx.x < x.world) {  // full gossip: the next plans' inputs
@@ -1346,15 +1352,15 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
     }
 }
 
-// hist[(src rank * world + dst rank) * 8 + degree] over every extra link (LDS-privatised).
-__global__ __launch_bounds__(kBlock) void k_link_hist(uint64_t seed, Geom g, Xchg x, unsigned long long* hist) {
-    __shared__ uint32_t h[kMaxWorld * kMaxWorld * 8];
-    const uint32_t nb = x.world * x.world * 8;
+// hist[(src piece * nd + dst rank) * 8 + degree] over every extra link (LDS-privatised).
+__global__ __launch_bounds__(kBlock) void k_link_hist(uint64_t seed, Geom g, HistBounds b, unsigned long long* hist) {
+    __shared__ uint32_t h[kMaxWorld * kMaxPieces * kMaxWorld * 8];
+    const uint32_t nb = b.ns * b.nd * 8;
     for (uint32_t i = threadIdx.x; i < nb; i += kBlock) h[i] = 0;
     __syncthreads();
     for (uint32_t u = blockIdx.x * kBlock + threadIdx.x; u < g.wired; u += gridDim.x * kBlock) {
-        const uint32_t sp = owner(x.abnd, x.world, u), dp = owner(x.abnd, x.world, link_of(seed, u, g.wired));
-        atomicAdd(&h[(sp * x.world + dp) * 8 + popc(presence(g, u))], 1u);
+        const uint32_t sp = owner(b.sb, b.ns, u), dp = owner(b.db, b.nd, link_of(seed, u, g.wired));
+        atomicAdd(&h[(sp * b.nd + dp) * 8 + popc(presence(g, u))], 1u);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nb; i += kBlock)
@@ -1441,7 +1447,7 @@ __device__ __forceinline__ void gs_push_body(const RoundArgs& a, const Xchg* xp)
 #pragma unroll
             for (uint32_t c = 0; c < 2; ++c) {
                 const bool send = tok > c;
-                remote[c] = send && (t[c] < a.lo || t[c] >= a.hi);
+                remote[c] = send && (t[c] < a.olo || t[c] >= a.ohi);
                 // local targets: the sender-side done filter of the single-GPU kernel
                 if (send && !remote[c] && !(a.gstate[t[c]] & 4u)) atomicAdd(&a.inc_cur[t[c]], 1u);
                 q[c] = remote[c] ? owner(x.abnd, x.world, t[c]) : 0u;
@@ -2520,8 +2526,8 @@ void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, u
     hipLaunchKernelGGL(k_shard_unpack, dim3(bpp * x.world), dim3(kBlock), 0, s, a, x, applied, gossip, full);
 }
 
-void launch_link_hist(uint64_t seed, const Geom& g, const Xchg& x, unsigned long long* hist, const Launch& l) {
-    hipLaunchKernelGGL(k_link_hist, dim3(l.grid), dim3(kBlock), 0, l.stream, seed, g, x, hist);
+void launch_link_hist(uint64_t seed, const Geom& g, const HistBounds& b, unsigned long long* hist, const Launch& l) {
+    hipLaunchKernelGGL(k_link_hist, dim3(l.grid), dim3(kBlock), 0, l.stream, seed, g, b, hist);
 }
 
 void launch_dst_count(uint64_t seed, uint32_t nodes, uint32_t ulo, uint32_t uhi, uint32_t* counts, const Launch& l) {

@@ -26,6 +26,8 @@ FLAG_GOSSIP_TALLY = 64
 FLAG_FULL_PLAN = 128
 FLAG_TIGHT_TIERS = 256
 FLAG_TALLY_FALLBACKS = 512
+FLAG_PIECES = 1024
+FLAG_FORCE_PIECES = 2048
 ERRORS = {-1: "GP_EINVAL", -2: "GP_ENOMEM", -3: "GP_EHIP", -4: "GP_ESTATE", -5: "GP_EOVERFLOW", -6: "GP_ERCCL"}
 
 
@@ -67,7 +69,8 @@ class ShardStats(C.Structure):
 EXPORTS = ["gp_abi_version", "gp_sizes", "gp_create", "gp_reset", "gp_step", "gp_read_gossip",
            "gp_read_pushsum", "gp_read_messages", "gp_read_trace", "gp_neighbors",
            "gp_kernel_stats", "gp_partition", "gp_create_shard", "gp_shard_plan", "gp_shard_round",
-           "gp_shard_deliver", "gp_shard_sync", "gp_shard_stats", "gp_destroy", "gp_last_error"]
+           "gp_shard_deliver", "gp_shard_sync", "gp_shard_stats", "gp_shard_pieces", "gp_shard_round_piece",
+           "gp_shard_plan_piece", "gp_destroy", "gp_last_error"]
 
 
 class GossipError(RuntimeError):
@@ -111,6 +114,9 @@ def load():
     L.gp_shard_deliver.argtypes = [P, P]
     L.gp_shard_sync.argtypes = [P, C.POINTER(Status)]
     L.gp_shard_stats.argtypes = [P, C.POINTER(ShardStats)]
+    L.gp_shard_pieces.argtypes = [P]
+    L.gp_shard_round_piece.argtypes = [P, P, C.c_int32]
+    L.gp_shard_plan_piece.argtypes = [P, C.c_int32, P, P, P]
     L.gp_destroy.argtypes = [P]
     L.gp_destroy.restype = None
     L.gp_last_error.restype = C.c_char_p

@@ -9,6 +9,10 @@ the actors on the .NET thread pool (program.fs:23), and the ParentActor counts r
     transport.exchange()    # ONE all-to-all (RCCL over xGMI); chunk sizes change only at a sync
     engine.deliver()        # unpack: halo faces, cross-shard link messages, global count
 
+or, for a large push-sum shard, the same round in pieces: the all-to-all of piece i
+runs (asynchronously, on the transport's own stream) while piece i+1 is computed, and the unpack
+waits for the last one.
+
 with everything enqueued on the engine's HIP stream — the host only waits every few rounds
 (``engine.sync()``) to learn whether the global completion count reached `nodes`.  At that sync
 a push-sum shard also sizes the next batch's chunks from the activity of the last one (activity
@@ -43,11 +47,13 @@ class HipShard:
     def __init__(self, n_arg: int, topology: str, algorithm: str, *, rank: int, world: int, seed: int = 1,
                  device: int = 0, stream: int | None = None, kernel_timing: bool = False, delta: float = 1e-10,
                  gossip_threshold: int = 10, term_init: int = 1, term_limit: int = 3, quiet_waves: bool = False,
-                 full_plan: bool = False, tight_tiers: bool = False):
+                 full_plan: bool = False, tight_tiers: bool = False, pieces: bool = True,
+                 force_pieces: bool = False):
         """quiet_waves: the push-sum quiet-tail walk at any shard size (a test hook; on by default
         for shards of 2^20 actors or more).  full_plan: no activity tiers (every round ships the
         all-sending capacity); tight_tiers: tiers with no headroom and frequent replays (a test
-        hook)."""
+        hook).  pieces: exchange a push-sum round piece by piece (the library picks 4 pieces from
+        2^20 actors per rank, else 1); force_pieces: 4 pieces at any size (a test hook)."""
         import torch
 
         if topology not in _abi.TOPOLOGIES:
@@ -60,6 +66,7 @@ class HipShard:
         flags = (_abi.FLAG_KERNEL_TIMING if kernel_timing else 0) | _abi.FLAG_USE_STREAM
         flags |= _abi.FLAG_QUIET_WAVES if quiet_waves else 0
         flags |= (_abi.FLAG_FULL_PLAN if full_plan else 0) | (_abi.FLAG_TIGHT_TIERS if tight_tiers else 0)
+        flags |= (_abi.FLAG_PIECES if pieces or force_pieces else 0) | (_abi.FLAG_FORCE_PIECES if force_pieces else 0)
         if stream is None:
             stream = torch.cuda.current_stream(device).cuda_stream
         self.cfg = _abi.Config(n_arg, _abi.TOPOLOGIES[topology], _abi.ALGOS[algorithm], seed, delta,
@@ -73,6 +80,7 @@ class HipShard:
         self.rank, self.world = rank, world
         self.topology, self.algorithm = topology, algorithm
         self.lo, self.hi = int(self.shard.lo), int(self.shard.hi)
+        self.npieces = int(self.lib.gp_shard_pieces(self.h))
         # full gossip sizes every round's chunks from the last round before a sync:
         # its host loop syncs every 4 rounds, so the plans follow the run's activity (its receipts
         # thin out by a third or more per round once targets report)
@@ -89,14 +97,29 @@ class HipShard:
     def _plan(self):
         """The next round's per-peer chunk sizes (gp_shard_plan): they follow the activity of the
         run (push-sum: per batch; full gossip: per round), so they are re-read after every round
-        and sync."""
+        and sync.  In pieces: piece_plans[i] = (send splits, recv splits, send offset, recv offset)
+        of piece i (gp_shard_plan_piece)."""
         if not hasattr(self, "_sb"):
             self._sb = np.zeros(self.world, np.int64)
             self._rb = np.zeros(self.world, np.int64)
+            self._ob = np.zeros(2, np.int64)
             self._sbp = self._sb.ctypes.data_as(C.c_void_p)
             self._rbp = self._rb.ctypes.data_as(C.c_void_p)
-        _abi.check(self.lib.gp_shard_plan(self.h, self._sbp, self._rbp))
-        self.send_splits, self.recv_splits = self._sb.tolist(), self._rb.tolist()
+            self._obp = self._ob.ctypes.data_as(C.c_void_p)
+        if self.npieces == 1:
+            _abi.check(self.lib.gp_shard_plan(self.h, self._sbp, self._rbp))
+            self.send_splits, self.recv_splits = self._sb.tolist(), self._rb.tolist()
+            self.piece_plans = [(self.send_splits, self.recv_splits, 0, 0)]
+            return
+        self.piece_plans = []
+        for i in range(self.npieces):
+            _abi.check(self.lib.gp_shard_plan_piece(self.h, i, self._sbp, self._rbp, self._obp))
+            self.piece_plans.append((self._sb.tolist(), self._rb.tolist(), int(self._ob[0]), int(self._ob[1])))
+        self.send_splits = self.recv_splits = None  # per piece only
+
+    def bytes_per_round(self):
+        """(send, receive) bytes of the current plan's whole round (every piece)."""
+        return (sum(sum(p[0]) for p in self.piece_plans), sum(sum(p[1]) for p in self.piece_plans))
 
     def shard_stats(self):
         s = _abi.ShardStats()
@@ -115,6 +138,10 @@ class HipShard:
     def round(self):
         _abi.check(self.lib.gp_shard_round(self.h, C.c_void_p(self.send_buf.data_ptr())))
         self._plan()  # this round's chunk sizes (the exchange that follows moves them)
+
+    def round_piece(self, i: int):
+        """Piece i of the round (in order); its exchange may start at once (piece_plans[i])."""
+        _abi.check(self.lib.gp_shard_round_piece(self.h, C.c_void_p(self.send_buf.data_ptr()), i))
 
     def deliver(self):
         _abi.check(self.lib.gp_shard_deliver(self.h, C.c_void_p(self.recv_buf.data_ptr())))
@@ -202,6 +229,18 @@ class TorchTransport:
         self.dist.all_to_all_single(eng.recv_buf[:nr], eng.send_buf[:ns], eng.recv_splits, eng.send_splits,
                                     group=self.group)
 
+    def exchange_piece(self, eng, i):
+        """Piece i's all-to-all, asynchronous: it waits for the kernels enqueued so far (piece i's)
+        and runs on the process group's stream while the next piece is computed; join() makes the
+        engine's stream wait for it."""
+        ss, rs, so, ro = eng.piece_plans[i]
+        return self.dist.all_to_all_single(eng.recv_buf[ro:ro + sum(rs)], eng.send_buf[so:so + sum(ss)], rs, ss,
+                                           group=self.group, async_op=True)
+
+    def join(self, works):
+        for w in works:
+            w.wait()
+
 
 def _offsets(splits):
     return np.concatenate([[0], np.cumsum(splits)]).astype(np.int64)
@@ -209,7 +248,36 @@ def _offsets(splits):
 
 class LoopbackTransport:
     """All shards live in this process (one GPU, or CPU): chunk p->q is copied from p's send
-    buffer into q's receive buffer (stream-ordered device copies for HipShard)."""
+    buffer into q's receive buffer (stream-ordered device copies for HipShard).  In pieces the
+    copies of piece i run on a stream of their own, after every shard's piece i, while the shards
+    compute piece i+1 (join: the engines' stream waits for the copies)."""
+
+    def __init__(self):
+        self.stream = None
+
+    def exchange_piece_all(self, engines, i):
+        import torch
+
+        if self.stream is None:
+            self.stream = torch.cuda.Stream()
+        self.stream.wait_stream(torch.cuda.current_stream())  # after every shard's piece i
+        with torch.cuda.stream(self.stream):
+            plans = [e.piece_plans[i] for e in engines]
+            so = [_offsets(pl[0]) + pl[2] for pl in plans]
+            ro = [_offsets(pl[1]) + pl[3] for pl in plans]
+            for p, ep in enumerate(engines):
+                for q, eq in enumerate(engines):
+                    n = plans[p][0][q]
+                    if p == q or n == 0:
+                        continue
+                    assert n == plans[q][1][p], (p, q, n, plans[q][1][p])
+                    eq.recv_buf[ro[q][p]:ro[q][p] + n].copy_(ep.send_buf[so[p][q]:so[p][q] + n])
+
+    def join(self):
+        import torch
+
+        if self.stream is not None:
+            torch.cuda.current_stream().wait_stream(self.stream)
 
     def exchange_all(self, engines):
         so = [_offsets(e.send_splits) for e in engines]
@@ -270,14 +338,24 @@ def run(engine, transport, max_rounds: int = 1 << 40, batch: int = 8, max_batch:
         # gossip's F(k) reports round k-1, so one more exchange than rounds is needed to learn
         # a convergence; rounds issued beyond it are no-ops on the device (gated).
         b = min(batch, goal - int(st.round))
+        pieces = getattr(engine, "npieces", 1)
         for _ in range(b):
             ev = timer.events() if timer else None
             if ev:
                 ev[0].record()
-            engine.round()
-            if ev:
-                ev[1].record()
-            transport.exchange(engine)
+            if pieces == 1:
+                engine.round()
+                if ev:
+                    ev[1].record()
+                transport.exchange(engine)
+            else:  # the exchange of piece i overlaps the kernels of piece i+1
+                works = []
+                for i in range(pieces):
+                    engine.round_piece(i)
+                    works.append(transport.exchange_piece(engine, i))
+                if ev:
+                    ev[1].record()  # every piece's kernels enqueued; "exchange": what is left of them
+                transport.join(works)
             if ev:
                 ev[2].record()
             engine.deliver()
@@ -319,10 +397,18 @@ def run_local(engines, max_rounds: int = 1 << 40, batch: int = 8, max_batch: int
     goal = int(sts[0].round) + max_rounds
     while not sts[0].converged and sts[0].round < goal:
         b = min(batch, goal - int(sts[0].round))
+        pieces = getattr(engines[0], "npieces", 1)
         for _ in range(b):
-            for e in engines:
-                e.round()
-            t.exchange_all(engines)
+            if pieces == 1:
+                for e in engines:
+                    e.round()
+                t.exchange_all(engines)
+            else:
+                for i in range(pieces):
+                    for e in engines:
+                        e.round_piece(i)
+                    t.exchange_piece_all(engines, i)
+                t.join()
             for e in engines:
                 e.deliver()
         before = int(sts[0].completed)

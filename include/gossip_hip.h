@@ -65,6 +65,13 @@ enum gp_flags {
                                   placement (a workgroup's receipts past its LDS) and the 32-bit
                                   escape of the 16-bit receipt words (counts >= 0xFFFF); a test
                                   hook, same results */
+    GP_FLAG_PIECES = 1024,     /* push-sum shards: the host exchanges each round piece by piece
+                                  (gp_shard_round_piece / gp_shard_plan_piece), so the exchange of
+                                  one piece overlaps the next piece's kernels; the library runs 4
+                                  pieces when every rank holds 2^20 actors or more, else 1
+                                  (gp_shard_pieces) */
+    GP_FLAG_FORCE_PIECES = 2048, /* with GP_FLAG_PIECES: 4 pieces at any size (whole z-planes, or
+                                  256 actors on line / 2D, permitting); a test hook, same results */
 };
 
 typedef struct gp_config {
@@ -195,8 +202,19 @@ int gp_create_shard(const gp_config* cfg, int32_t rank, int32_t world, gp_layout
  * gp_shard_round.  Both ends of a chunk always agree on its size. */
 int gp_shard_plan(void* handle, int64_t* send_bytes, int64_t* recv_bytes);
 /* Enqueue one round on the handle's stream and pack what other ranks need into send_buf
- * (device memory, send_total bytes, 256-byte aligned).  Asynchronous. */
+ * (device memory, send_total bytes, 256-byte aligned).  Asynchronous.  (In pieces: every piece in
+ * turn, for a host that exchanges the round's pieces one after another afterwards.) */
 int gp_shard_round(void* handle, void* send_buf);
+/* A round in pieces (GP_FLAG_PIECES, ABI 6).  gp_shard_pieces: the pieces per round
+ * (1: gp_shard_round / gp_shard_plan as above).  Piece i of a round is gp_shard_round_piece(h, send,
+ * i), i = 0 .. pieces-1 in order, each followed by its own all-to-all of the per-peer sizes
+ * gp_shard_plan_piece gives, at offsets[0] of the send buffer and offsets[1] of the receive buffer
+ * (pieces are laid out one after another); the exchange of piece i runs while piece i+1 is computed.
+ * gp_shard_deliver follows the last piece's exchange.  gp_shard_plan fails with GP_ESTATE when the
+ * round runs in pieces. */
+int gp_shard_pieces(void* handle);
+int gp_shard_round_piece(void* handle, void* send_buf, int32_t piece);
+int gp_shard_plan_piece(void* handle, int32_t piece, int64_t* send_bytes, int64_t* recv_bytes, int64_t* offsets);
 /* Enqueue the unpacking of what the other ranks sent for that round (recv_buf: recv_total
  * bytes of device memory).  Must follow each gp_shard_round.  Asynchronous. */
 int gp_shard_deliver(void* handle, const void* recv_buf);

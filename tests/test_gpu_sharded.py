@@ -229,7 +229,7 @@ def test_shards_activity_tiers_default():
     ref = Simulator(n, "Imp3D", "push-sum", seed=seed)
     rs = ref.step()
     engines = _shards(n, "Imp3D", "push-sum", 8, seed)
-    full_bytes = sum(engines[0].send_splits)
+    full_bytes = engines[0].bytes_per_round()[0]
     t = sharded.LoopbackTransport()
     sts = [e.sync() for e in engines]
     least, batch = full_bytes, 8
@@ -241,7 +241,7 @@ def test_shards_activity_tiers_default():
             for e in engines:
                 e.deliver()
         sts = [e.sync() for e in engines]
-        least = min(least, sum(engines[0].send_splits))
+        least = min(least, engines[0].bytes_per_round()[0])
         batch = min(batch * 2, 64)
     assert (sts[0].round, sts[0].completed) == (rs.round, rs.completed)
     _check_vs(ref, engines, "push-sum")
@@ -337,11 +337,58 @@ def test_group_tight_tiers_vs_oracle(n, topo, world, seed):
     cpu.close()
 
 
+# Rounds in pieces, forced at small sizes: each piece's round kernel and link pass
+# over its own actors, the halo faces in the end pieces, its headers and chunks, exchanged piece by
+# piece on the loopback transport's own stream; the quiet tail walks each piece's segments.
+PIECE_CASES = [(1000, "Imp3D", 2, 1, None), (20000, "Imp3D", 3, 5, None), (300000, "Imp3D", 8, 11, None),
+               (8000, "3D", 4, 2, None), (20000, "line", 3, 4, 400), (40000, "2D", 2, 6, 400)]
+
+
+@pytest.mark.parametrize("tiers", ["default", "tight"])
+@pytest.mark.parametrize("n,topo,world,seed,cap", PIECE_CASES)
+def test_shards_pieces_vs_oracle(n, topo, world, seed, cap, tiers):
+    """tight: the per-(piece, peer) activity tiers overflow and replay from restore points."""
+    ref = oracle.OracleSim(n, topo, "push-sum", seed=seed)
+    rs = ref.step(cap or 1 << 20, threads=8)
+    engines = _shards(n, topo, "push-sum", world, seed, quiet_waves=True, force_pieces=True,
+                      tight_tiers=tiers == "tight")
+    assert all(e.npieces == 4 for e in engines), [e.npieces for e in engines]
+    sts = sharded.run_local(engines, max_rounds=int(rs.round))
+    for st in sts:
+        assert (st.round, st.completed, st.converged) == (rs.round, rs.completed, rs.converged)
+    _check_vs(ref, engines, "push-sum")
+    if tiers == "tight" and n >= 20000 and cap is None:
+        assert sum(e.shard_stats()["restores"] for e in engines) > 0
+    for e in engines:
+        e.close()
+
+
+def test_group_pieces_vs_oracle():
+    """The library's multi-GPU engine in pieces: each piece's exchange on the group's own stream
+    (one device: copies), joined before the unpacks."""
+    n, world, seed = 100000, 4, 3
+    gpu = Simulator(n, "Imp3D", "push-sum", seed=seed, num_gpus=world, one_device=True, quiet_waves=True,
+                    force_pieces=True)
+    cpu = oracle.OracleSim(n, "Imp3D", "push-sum", seed=seed)
+    gs, cs = gpu.step(), cpu.step(1 << 20, threads=8)
+    assert gs.converged and (gs.round, gs.completed) == (cs.round, cs.completed)
+    S, W, f = gpu.read_pushsum()
+    rS, rW, rf = cpu.read_pushsum()
+    np.testing.assert_array_equal(f, rf)
+    np.testing.assert_array_equal(bits(S), bits(rS))
+    np.testing.assert_array_equal(bits(W), bits(rW))
+    np.testing.assert_array_equal(gpu.read_trace(), cpu.read_trace())
+    gpu.close()
+    cpu.close()
+
+
 def test_shards_imp3d_10m_two_ranks():
-    """BASELINE config 3 split over 2 shards: the same run as the single-GPU engine."""
+    """BASELINE config 3 split over 2 shards (in 4 pieces each: 5M actors per rank): the same run as
+    the single-GPU engine."""
     ref = Simulator(10_000_000, "Imp3D", "push-sum", seed=1)
     rs = ref.step()
     engines = _shards(10_000_000, "Imp3D", "push-sum", 2, seed=1)
+    assert all(e.npieces == 4 for e in engines)
     sts = sharded.run_local(engines)
     assert rs.converged and (sts[0].round, sts[0].completed) == (rs.round, rs.completed)
     np.testing.assert_array_equal(engines[0].read_trace(), ref.read_trace())

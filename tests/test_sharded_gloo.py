@@ -35,7 +35,52 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, case, bounds, q):
+class PiecedOracle:
+    """The oracle's shard engine behind the piece API of HipShard (npieces, round_piece, piece_plans):
+    each round's chunk p -> q is cut into K byte ranges, laid out piece-major as the library lays out
+    its pieces, and moved by K all-to-alls (TorchTransport.exchange_piece / join), which the host loop
+    (sharded.run) issues one per piece.  Checks the piece transport and loop on CPU."""
+
+    def __init__(self, eng, K):
+        import torch
+
+        self.e, self.npieces, self.layout = eng, K, eng.layout
+        so = np.concatenate([[0], np.cumsum(eng.send_splits)])
+        ro = np.concatenate([[0], np.cumsum(eng.recv_splits)])
+        self.piece_plans, self.smap, self.rmap = [], [], []
+        sb = rb = 0
+        for i in range(K):
+            ss = [n * (i + 1) // K - n * i // K for n in eng.send_splits]
+            rs = [n * (i + 1) // K - n * i // K for n in eng.recv_splits]
+            self.piece_plans.append((ss, rs, sb, rb))
+            for q, n in enumerate(eng.send_splits):
+                self.smap.append((sb, int(so[q]) + n * i // K, ss[q]))
+                sb += ss[q]
+            for q, n in enumerate(eng.recv_splits):
+                self.rmap.append((rb, int(ro[q]) + n * i // K, rs[q]))
+                rb += rs[q]
+        self.send_buf = torch.zeros(sb, dtype=torch.uint8)
+        self.recv_buf = torch.zeros(rb, dtype=torch.uint8)
+
+    def round_piece(self, i):
+        if i == 0:  # the oracle computes the round whole; piece i only moves bytes
+            self.e.round()
+            for dst, src, n in self.smap:
+                self.send_buf[dst:dst + n] = self.e.send_buf[src:src + n]
+
+    def deliver(self):
+        for src, dst, n in self.rmap:
+            self.e.recv_buf[dst:dst + n] = self.recv_buf[src:src + n]
+        self.e.deliver()
+
+    def sync(self):
+        return self.e.sync()
+
+    def __getattr__(self, name):  # read_*, lo, hi, ...
+        return getattr(self.e, name)
+
+
+def _worker(rank, world, port, case, bounds, q, pieces=1):
     for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "cop5615-gossip_protocol_amd")):
         sys.path.insert(0, p)
     import torch.distributed as dist
@@ -47,6 +92,8 @@ def _worker(rank, world, port, case, bounds, q):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         eng = oracle.OracleShard(n, topo, algo, rank=rank, world=world, bounds=bounds, seed=seed)
+        if pieces > 1:
+            eng = PiecedOracle(eng, pieces)
         st = sharded.run(eng, sharded.TorchTransport(), max_rounds=cap)
         state = eng.read_gossip() if algo == "gossip" else eng.read_pushsum()
         sums = None
@@ -61,11 +108,11 @@ def _worker(rank, world, port, case, bounds, q):
         dist.destroy_process_group()
 
 
-def _run_job(case, world, bounds):
+def _run_job(case, world, bounds, pieces=1):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, bounds, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, bounds, q, pieces)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=240) for _ in range(world)]
@@ -77,7 +124,7 @@ def _run_job(case, world, bounds):
 
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[2]}-{c[1]}-{c[0]}")
-def test_sharded_matches_single_process(case, world):
+def test_sharded_matches_single_process(case, world, pieces=1):
     import oracle
     from gossip_amd import sharded
 
@@ -87,7 +134,7 @@ def test_sharded_matches_single_process(case, world):
     rs = ref.step(cap)
     ref_state = ref.read_gossip() if algo == "gossip" else ref.read_pushsum()
     ref_trace = ref.read_trace()
-    out = _run_job(case, world, bounds)
+    out = _run_job(case, world, bounds, pieces)
     for rank, rnd, comp, conv, trace, state, sums in out:
         assert (rnd, comp, conv) == (rs.round, rs.completed, rs.converged), (rank, rnd, rs.round)
         np.testing.assert_array_equal(trace, ref_trace)
@@ -105,6 +152,16 @@ def test_sharded_matches_single_process(case, world):
 def test_sharded_world8(case):
     """The driver's rank count (8 processes over gloo): the same host loop and transport."""
     test_sharded_matches_single_process(case, 8)
+
+
+@pytest.mark.parametrize("world,pieces", [(2, 4), (3, 3)])
+@pytest.mark.parametrize("case", [(1000, "Imp3D", "push-sum", 1, 4000), (200, "line", "push-sum", 2, 300)],
+                         ids=lambda c: f"{c[2]}-{c[1]}-{c[0]}")
+def test_sharded_pieces_gloo(case, world, pieces):
+    """A round in pieces through the product host loop: one asynchronous
+    all-to-all per piece (TorchTransport.exchange_piece, joined before the unpack), bit-exact
+    against one process."""
+    test_sharded_matches_single_process(case, world, pieces)
 
 
 def test_uneven_partition_gossip_full():

@@ -28,6 +28,7 @@ ap.add_argument("--algorithm", default="push-sum")
 ap.add_argument("--rounds", type=int, default=None, help="default: to convergence")
 ap.add_argument("--seed", type=int, default=1)
 ap.add_argument("--series", default=None, help="write the per-round series (JSON) here")
+ap.add_argument("--no-pieces", action="store_true", help="one piece per round (no exchange overlap)")
 a = ap.parse_args()
 
 import torch  # noqa: E402
@@ -35,8 +36,9 @@ import torch  # noqa: E402
 from gossip_amd import sharded  # noqa: E402
 
 torch.cuda.set_device(0)
-shards = [sharded.HipShard(a.n, a.topology, a.algorithm, rank=r, world=a.world, seed=a.seed, kernel_timing=True)
-          for r in range(a.world)]
+shards = [sharded.HipShard(a.n, a.topology, a.algorithm, rank=r, world=a.world, seed=a.seed, kernel_timing=True,
+                           pieces=not a.no_pieces) for r in range(a.world)]
+K = shards[0].npieces
 nodes = shards[0].nodes
 sharded.run_local(shards, max_rounds=8)  # warm-up (module load, first touches)
 for e in shards:
@@ -47,35 +49,40 @@ cap = a.rounds if a.rounds else 1 << 40
 t = sharded.LoopbackTransport()
 events = []
 sts = [e.sync() for e in shards]
-send_bytes = [(0, sum(shards[0].send_splits))]
+send_bytes = [(0, shards[0].bytes_per_round()[0])]
 round_bytes = []  # rank 0's send bytes per round (full gossip plans every round)
 max_batch = sharded._max_batch(shards[0], 64)
 batch = min(8, max_batch)
 t0 = time.perf_counter()
 while not sts[0].converged and sts[0].round < cap:
     for _ in range(min(batch, cap - int(sts[0].round))):
-        # the whole round, and rank 0's own work in it: its round kernels + passes, the chunk
-        # copies of every rank, its unpack
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        # the whole round on the shards' stream: every rank's round kernels and passes (in pieces:
+        # each piece's chunk copies on the transport's own stream, overlapping the next piece), what
+        # is left of the copies after the last piece (joined), every rank's unpack
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         ev[0].record()
-        for i, e in enumerate(shards):
-            e.round()
-            if i == 0:
-                ev[1].record()
-        round_bytes.append(sum(shards[0].send_splits))  # rank 0's chunks of this round
+        if K == 1:
+            for e in shards:
+                e.round()
+            ev[1].record()
+            t.exchange_all(shards)
+        else:
+            for i in range(K):
+                for e in shards:
+                    e.round_piece(i)
+                t.exchange_piece_all(shards, i)
+            ev[1].record()
+            t.join()
+        round_bytes.append(shards[0].bytes_per_round()[0])  # rank 0's chunks of this round
         ev[2].record()
-        t.exchange_all(shards)
-        ev[3].record()
-        for i, e in enumerate(shards):
+        for e in shards:
             e.deliver()
-            if i == 0:
-                ev[4].record()
-        ev[5].record()
+        ev[3].record()
         events.append(ev)
     before = int(sts[0].completed)
     sts = [e.sync() for e in shards]
     assert len({(int(s.round), int(s.completed), int(s.converged)) for s in sts}) == 1, "shards disagree"
-    send_bytes.append((int(sts[0].round), sum(shards[0].send_splits)))  # rank 0's plan from here on
+    send_bytes.append((int(sts[0].round), shards[0].bytes_per_round()[0]))  # rank 0's plan from here on
     batch = sharded._next_batch(batch, max_batch, nodes, before, int(sts[0].completed))  # the product loop's schedule
 torch.cuda.synchronize()
 el = time.perf_counter() - t0
@@ -84,10 +91,12 @@ trace = [int(x) for x in shards[0].read_trace()]
 # gossip's F(k) applies round k - 1: one launch more than rounds
 launches = rounds + (1 if a.algorithm == "gossip" else 0)
 nl = min(launches, len(events))
-per_round = [events[i][0].elapsed_time(events[i][5]) for i in range(nl)]
-# rank 0 without the transport: its round (kernel + passes + pack) and its unpack
-rank0 = [events[i][0].elapsed_time(events[i][1]) + events[i][3].elapsed_time(events[i][4]) for i in range(nl)]
-copies = [events[i][2].elapsed_time(events[i][3]) for i in range(nl)]
+per_round = [events[i][0].elapsed_time(events[i][3]) for i in range(nl)]
+# the phases of a round on the shards' stream (all ranks): the round kernels and passes (in pieces
+# the copies of all but the last piece run beside them), the copies not hidden, the unpacks
+compute = [events[i][0].elapsed_time(events[i][1]) for i in range(nl)]
+copies = [events[i][1].elapsed_time(events[i][2]) for i in range(nl)]
+unpack = [events[i][2].elapsed_time(events[i][3]) for i in range(nl)]
 ks = shards[0].kernel_stats()
 
 
@@ -115,10 +124,13 @@ summary = {
     "rank_round_ms_dense": phase(per_round, dense_r, a.world),
     "rank_round_ms_tail": phase(per_round, tail_r, a.world),
     "tail_over_dense": phase(per_round, tail_r) / phase(per_round, dense_r) if dense_r and tail_r else None,
-    # rank 0's own kernels per round (no transport: on a real node its all-to-all runs in parallel)
-    "rank0_ms_dense": phase(rank0, dense_r), "rank0_ms_tail": phase(rank0, tail_r),
-    "rank0_tail_over_dense": phase(rank0, tail_r) / phase(rank0, dense_r) if dense_r and tail_r else None,
-    "copies_ms_dense": phase(copies, dense_r), "copies_ms_tail": phase(copies, tail_r),
+    # per rank-round (all ranks / world): round kernels and passes, the copies left exposed after
+    # the last piece (in pieces; else all of them), the unpack
+    "pieces": K,
+    "compute_ms_dense": phase(compute, dense_r, a.world), "exposed_copies_ms_dense": phase(copies, dense_r, a.world),
+    "unpack_ms_dense": phase(unpack, dense_r, a.world),
+    "compute_ms_tail": phase(compute, tail_r, a.world), "exposed_copies_ms_tail": phase(copies, tail_r, a.world),
+    "unpack_ms_tail": phase(unpack, tail_r, a.world),
     "rank0_kernel": ks["kernel"], "rank0_kernel_avg_ms": ks["avg_ms"], "rank0_aux": ks["aux_kernel"],
     "rank0_aux_avg_ms": ks["aux_avg_ms"], "rank0_work_per_launch": ks["work_per_launch"],
     "rank0_actors": shards[0].hi - shards[0].lo,
@@ -133,7 +145,8 @@ print(json.dumps(summary, indent=1), flush=True)
 if a.series:
     with open(a.series, "w") as f:
         json.dump(dict(summary, per_round_ms=[round(x, 4) for x in per_round],
-                       rank0_ms=[round(x, 4) for x in rank0], copies_ms=[round(x, 4) for x in copies],
+                       compute_ms=[round(x, 4) for x in compute], copies_ms=[round(x, 4) for x in copies],
+                       unpack_ms=[round(x, 4) for x in unpack],
                        send_bytes=send_bytes, round_bytes=round_bytes, trace=trace), f)
 for e in shards:
     e.close()
