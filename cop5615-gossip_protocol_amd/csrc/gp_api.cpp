@@ -155,8 +155,13 @@ struct Handle {
     // A round in pieces: piece i of every rank's range is computed, packed and
     // exchanged on its own, so the exchange of one piece overlaps the next piece's kernels.  Chunks
     // are per (piece, peer), index i * world + q, laid out piece-major in the buffers.
-    int npiece = 1;
-    std::vector<int64_t> pbnd;                // piece bounds of every rank: pbnd[q * (npiece + 1) + i]
+    // The pieces run while the exchange carries the full plan (until half the nodes have converged;
+    // after that the activity tiers shrink it and the extra launches would cost more than they hide):
+    // kpiece is the handle's piece count, npiece the current one (1 or kpiece, chosen at a sync from
+    // the global count, so every rank agrees).
+    int kpiece = 1, npiece = 1;
+    std::vector<int64_t> pbnd;                // kpiece bounds of every rank: pbnd[q * (kpiece + 1) + i]
+    std::vector<Chunk> full_by[2][2];         // full plans [npiece > 1][out, in]
     int piece_next = 0;                       // the next piece gp_shard_round_piece packs
     int64_t round_slot = -1;                  // timing slot of the round being packed (-1: untimed)
     std::vector<unsigned long long> lhist;    // (src piece, dst rank, degree) link counts
@@ -289,7 +294,10 @@ struct Handle {
     int64_t ext_lo() const { return std::max<int64_t>(0, (int64_t)lo - halo); }
     int64_t ext_hi() const { return std::min<int64_t>(g.actors, (int64_t)hi + halo); }
     uint32_t own() const { return hi - lo; }
-    int64_t piece_lo(int q, int i) const { return pbnd[(size_t)q * (npiece + 1) + i]; }
+    int64_t piece_lo(int q, int i) const {
+        if (npiece == 1) return i == 0 ? abnd[q] : abnd[q + 1];
+        return pbnd[(size_t)q * (kpiece + 1) + i];
+    }
 
     Launch L() const { return Launch{grid, stream}; }
 
@@ -455,13 +463,13 @@ int build_links(Handle* h) {
         }
     }
     if (h->sharded) {  // link counts per (source piece, destination rank, sender degree)
-        const int K = h->npiece, W = h->world;
+        const int K = h->kpiece, W = h->world;
         const size_t nb = (size_t)W * K * W * 8;
         HistBounds hb{};
         hb.ns = (uint32_t)(W * K);
         hb.nd = (uint32_t)W;
         for (int q = 0; q < W; ++q)
-            for (int i = 0; i < K; ++i) hb.sb[q * K + i] = (uint32_t)h->piece_lo(q, i);
+            for (int i = 0; i < K; ++i) hb.sb[q * K + i] = (uint32_t)h->pbnd[(size_t)q * (K + 1) + i];
         hb.sb[W * K] = (uint32_t)h->abnd[W];
         for (int q = 0; q <= W; ++q) hb.db[q] = (uint32_t)h->abnd[q];
         unsigned long long* hist = nullptr;
@@ -518,6 +526,8 @@ size_t dsum_words_all(const Handle* h) { return ((size_t)h->g.actors + 1023u) / 
 size_t dship_words(const Handle* h) { return (size_t)(((h->hi - 1u) >> 5) - (h->lo >> 5) + 1u); }
 
 void full_plan(Handle* h);
+void use_layout(Handle* h, int K);
+int want_pieces(const Handle* h);
 bool tiers_on(const Handle* h);
 bool gossip_plans(const Handle* h);
 void gossip_round_plan(Handle* h, int64_t k);
@@ -611,6 +621,7 @@ int reset(Handle* h) {
         h->full_until = 0;
         h->last_recv = nullptr;
         h->bytes_sent = 0;
+        if (h->kpiece > 1 && !h->full_out.empty()) use_layout(h, want_pieces(h));
         if (!h->full_out.empty()) full_plan(h);
         if (gossip_plans(h) && !h->full_out.empty()) {
             // round 0's chains: the leader's one (program.fs:218); the sized plans run from round 0, so
@@ -1045,7 +1056,10 @@ Chunk chunk_layout(const Handle* h, int p, int q, int i) {
         exact = chains;  // one sub-segment's bound
     } else if (h->g.has_link) {
         for (int d = 1; d < 8; ++d) {
-            const double n = (double)h->lhist[(((size_t)p * h->npiece + i) * h->world + q) * 8 + d];
+            // the link counts are per piece of kpiece; the round's only piece holds them all
+            double n = 0.0;
+            for (int j = h->npiece > 1 ? i : 0; j < (h->npiece > 1 ? i + 1 : h->kpiece); ++j)
+                n += (double)h->lhist[(((size_t)p * h->kpiece + j) * h->world + q) * 8 + d];
             const double pick = h->gossip ? 1.0 - (1.0 - 1.0 / d) * (1.0 - 1.0 / d) : 1.0 / d;
             mean += n * pick;
             exact += n;
@@ -1095,11 +1109,13 @@ void full_plan(Handle* h) {
     apply_plan(h, o, i);
 }
 
-int build_plan(Handle* h) {
-    const int W = h->world, p = h->rank, K = h->npiece;
+// The full plan of a round in K pieces (1 or kpiece) becomes the current layout.
+void use_layout(Handle* h, int K) {
+    const int W = h->world;
     const size_t n = (size_t)K * W;
-    h->full_out.assign(n, Chunk{});
-    h->full_in.assign(n, Chunk{});
+    h->npiece = K;
+    h->full_out = h->full_by[K > 1][0];
+    h->full_in = h->full_by[K > 1][1];
     h->out_chunk.assign(n, Chunk{});
     h->in_chunk.assign(n, Chunk{});
     h->out_off.assign(n, 0);
@@ -1107,15 +1123,36 @@ int build_plan(Handle* h) {
     h->out_poff.assign((size_t)K + 1, 0);
     h->in_poff.assign((size_t)K + 1, 0);
     h->max_in_cap.assign((size_t)K, 0u);
-    for (int i = 0; i < K; ++i)
-        for (int q = 0; q < W; ++q)
-            if (q != p) {
-                h->full_out[(size_t)i * W + q] = chunk_layout(h, p, q, i);
-                h->full_in[(size_t)i * W + q] = chunk_layout(h, q, p, i);
-            }
     full_plan(h);
-    h->send_total = h->out_poff[K];
-    h->recv_total = h->in_poff[K];
+}
+
+// Pieces while the run is before half its nodes converged (the full plan's exchange), one piece after.
+int want_pieces(const Handle* h) {
+    return h->kpiece > 1 && !h->converged && h->completed * 2 < h->lay.nodes ? h->kpiece : 1;
+}
+
+int build_plan(Handle* h) {
+    const int W = h->world, p = h->rank;
+    int64_t st = 0, rt = 0;
+    for (int K : {1, h->kpiece}) {
+        h->npiece = K;
+        std::vector<Chunk>& fo = h->full_by[K > 1][0];
+        std::vector<Chunk>& fi = h->full_by[K > 1][1];
+        fo.assign((size_t)K * W, Chunk{});
+        fi.assign((size_t)K * W, Chunk{});
+        for (int i = 0; i < K; ++i)
+            for (int q = 0; q < W; ++q)
+                if (q != p) {
+                    fo[(size_t)i * W + q] = chunk_layout(h, p, q, i);
+                    fi[(size_t)i * W + q] = chunk_layout(h, q, p, i);
+                }
+        use_layout(h, K);
+        st = std::max(st, h->out_poff[K]);  // the buffers hold either layout's full plan
+        rt = std::max(rt, h->in_poff[K]);
+        if (h->kpiece == 1) break;
+    }
+    h->send_total = st;
+    h->recv_total = rt;
     int rc;
     if ((rc = h->alloc(&h->pcount, ((size_t)W + 2) * kSub * kCtrStride)) || (rc = h->alloc(&h->overflow, 1)) ||
         (rc = h->alloc(&h->self_newly, 1)) || (rc = h->alloc(&h->pmax, (size_t)kMaxPieces * kMaxWorld)))
@@ -1484,6 +1521,7 @@ int restore(Handle* h, int64_t reached) {
     ++h->restores;
     h->tiered = false;
     h->delivered = 0;
+    if (h->kpiece > 1) use_layout(h, want_pieces(h));
     full_plan(h);
     return GP_OK;
 }
@@ -1494,10 +1532,12 @@ int choose_plan(Handle* h) {
     // rank's were reset, the peers' last headers were not)
     if (!h->delivered) return GP_OK;
     h->delivered = 0;
-    const int W = h->world, K = h->npiece;
-    const size_t n = (size_t)K * W;
+    const int W = h->world, K0 = h->npiece;
     const bool tight = (h->cfg.flags & GP_FLAG_TIGHT_TIERS) != 0;
-    // per (piece, peer): this rank's running maxima, and the peers' from the headers they sent last
+    // per (piece, peer) of the batch just run: this rank's running maxima, and the peers' from the
+    // headers they sent last
+    int K = K0;
+    size_t n = (size_t)K * W;
     std::vector<uint32_t> pm((size_t)kMaxPieces * kMaxWorld, 0u), mo(n, 0u), mi(n, 0u);
     HIP_TRY(hipMemcpy(pm.data(), h->pmax, pm.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
     for (int i = 0; i < K; ++i)
@@ -1509,6 +1549,28 @@ int choose_plan(Handle* h) {
                                   sizeof(uint32_t), hipMemcpyDeviceToHost));
         }
     HIP_TRY(hipMemsetAsync(h->pmax, 0, (size_t)kMaxPieces * kMaxWorld * sizeof(uint32_t), h->stream));
+    // the pieces of the next batch (a global decision); the counts carry over: a round's pieces
+    // held together at most the sum of their counts, and one piece at most the whole round's
+    if (want_pieces(h) != K0) {
+        K = want_pieces(h);
+        const size_t n1 = (size_t)K * W;
+        std::vector<uint32_t> mo1(n1, 0u), mi1(n1, 0u);
+        for (int i = 0; i < std::max(K, K0); ++i)
+            for (int q = 0; q < W; ++q) {
+                const size_t c0 = (size_t)(K0 > 1 ? i : 0) * W + q, c1 = (size_t)(K > 1 ? i : 0) * W + q;
+                if (K > 1) {  // every piece as much as the whole round
+                    mo1[c1] = mo[c0];
+                    mi1[c1] = mi[c0];
+                } else {
+                    mo1[c1] += mo[c0];
+                    mi1[c1] += mi[c0];
+                }
+            }
+        mo.swap(mo1);
+        mi.swap(mi1);
+        n = n1;
+        use_layout(h, K);
+    }
     // global conditions only (every rank decides alike): half the nodes converged (the tail), no
     // replay in progress, a batch already run
     const bool on = !h->converged && h->last_recv && h->rounds >= h->full_until &&
@@ -1609,8 +1671,10 @@ int shard_sync(Handle* h, gp_status* st) {
     h->timed_count = 0;
     if (gossip_plans(h)) {
         if ((rc = gossip_sync(h))) return rc;
-    } else if (tiers_on(h) && (rc = choose_plan(h))) {
-        return rc;
+    } else if (tiers_on(h)) {
+        if ((rc = choose_plan(h))) return rc;  // (the pieces of the next batch too)
+    } else if (h->kpiece > 1 && want_pieces(h) != h->npiece) {
+        use_layout(h, want_pieces(h));
     }
     if (st) {
         std::memset(st, 0, sizeof *st);
@@ -1707,13 +1771,13 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
             units = std::min(units, (bounds[q + 1] - bounds[q]) / unit);
         }
         const bool big = least >= kPieceMinActors || (cfg->flags & GP_FLAG_FORCE_PIECES);
-        h->npiece = big && units >= kMaxPieces ? kMaxPieces : 1;
+        h->kpiece = h->npiece = big && units >= kMaxPieces ? kMaxPieces : 1;
     }
-    h->pbnd.assign((size_t)h->world * (h->npiece + 1), 0);
+    h->pbnd.assign((size_t)h->world * (h->kpiece + 1), 0);
     for (int q = 0; q < h->world; ++q) {
         const int64_t unit = g.gz > 1 ? (int64_t)g.plane : 256, n = (bounds[q + 1] - bounds[q]) / unit;
-        for (int i = 0; i <= h->npiece; ++i)
-            h->pbnd[(size_t)q * (h->npiece + 1) + i] = i == h->npiece ? bounds[q + 1] : bounds[q] + n * i / h->npiece * unit;
+        for (int i = 0; i <= h->kpiece; ++i)
+            h->pbnd[(size_t)q * (h->kpiece + 1) + i] = i == h->kpiece ? bounds[q + 1] : bounds[q] + n * i / h->kpiece * unit;
     }
     // leader = Random().Next(0, nodes)  (program.fs:173/211/250/316)
     h->lay.leader = scale_draw(philox(0u, 0u, kStreamLeader, cfg->seed).x, (uint32_t)nodes);
@@ -2169,7 +2233,7 @@ int group_create(const gp_config* cfg, gp_layout* out, void** handle) {
         bytes += lay.device_bytes + s->send_total + s->recv_total;
         if (p == 0) h->lay = lay;
     }
-    if (G.shard[0]->npiece > 1) {  // the exchange streams and events of the pieces
+    if (G.shard[0]->kpiece > 1) {  // the exchange streams and events of the pieces
         G.xstream.assign((size_t)W, nullptr);
         G.ev_done.assign((size_t)W, nullptr);
         G.ev_x.assign((size_t)W, nullptr);

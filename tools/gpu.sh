@@ -32,7 +32,11 @@ kt() {  # $1 = output name, rest = command
   local n=$1; shift
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 ${KT_TIMEOUT:-240} rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$n" -o kt -- "$@" > "$O/$n.log" 2>&1 )
   rc=$?; echo "kt $n rc=$rc"; tail -1 "$O/$n.log"; [ $rc -eq 0 ] || return $rc
-  python3 "$R/tools/kt_summary.py" "$O/$n/kt_kernel_trace.csv" > "$O/$n.summary" && head -n ${KT_LINES:-6} "$O/$n.summary"
+  python3 "$R/tools/kt_summary.py" "$O/$n/kt_kernel_trace.csv" > "$O/$n.summary" && head -n ${KT_LINES:-6} "$O/$n.summary" || return $?
+  # KT_POST: a command run on the trace before it is dropped (KT_DROP=1: the trace CSV is too big to
+  # travel back, gpurun merges 64 MiB at most)
+  if [ -n "$KT_POST" ]; then eval "$KT_POST" > "$O/$n.post" 2>&1; cat "$O/$n.post"; fi
+  if [ "${KT_DROP:-0}" = 1 ]; then rm -f "$O/$n/kt_kernel_trace.csv"; fi
 }
 case $MODE in
   tests) tests ;;

@@ -1,10 +1,12 @@
 """Per-kernel cost of one rank-round by phase of a loopback shard run (tools/shard_loopback_prof.py
 under rocprofv3 --kernel-trace): the dispatches are assigned to rounds by counting the round
-kernel's launches (world per round, after the 8 warm-up rounds), and each round to a phase by the
-global completion count before it (the run's trace from --series).
+kernel's launches (world per round, or world x pieces for a round in pieces, after the 8 warm-up
+rounds), and each round to a phase by the global completion count before it (the run's trace from
+--series).
 
     python3 tools/loop_phase_kernels.py KT_CSV SERIES_JSON ROUND_KERNEL [world]
 """
+import bisect
 import csv
 import json
 import statistics
@@ -22,13 +24,22 @@ def main():
     d = json.load(open(series))
     trace, nodes = d["trace"], None
     rows = sorted(csv.DictReader(open(kt)), key=lambda r: int(r["Start_Timestamp"]))
+    # launches of the round kernel per round: world x the round's pieces (8 warm-up rounds first)
+    pieces = [d.get("warmup_pieces", 1)] * 8 + d.get("pieces_per_round", [])
+    starts, acc = [], 0
+    for k in pieces:
+        starts.append(acc)
+        acc += world * k
     seen, rnd = 0, -1
     per = defaultdict(lambda: defaultdict(float))  # round -> kernel -> us (all ranks)
     for r in rows:
         n = name(r)
         if n == rk:
+            if seen < acc:
+                rnd = bisect.bisect_right(starts, seen) - 1 - 8
+            else:  # launched past the recorded rounds (one piece each)
+                rnd = len(pieces) - 8 + (seen - acc) // world
             seen += 1
-            rnd = (seen - 1) // world - 8  # 8 warm-up rounds
         if rnd < 0:
             continue
         per[rnd][n] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3

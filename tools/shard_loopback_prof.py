@@ -38,7 +38,8 @@ from gossip_amd import sharded  # noqa: E402
 torch.cuda.set_device(0)
 shards = [sharded.HipShard(a.n, a.topology, a.algorithm, rank=r, world=a.world, seed=a.seed, kernel_timing=True,
                            pieces=not a.no_pieces) for r in range(a.world)]
-K = shards[0].npieces
+pieces_per_round = []
+warmup_pieces = shards[0].npieces
 nodes = shards[0].nodes
 sharded.run_local(shards, max_rounds=8)  # warm-up (module load, first touches)
 for e in shards:
@@ -61,6 +62,8 @@ while not sts[0].converged and sts[0].round < cap:
         # is left of the copies after the last piece (joined), every rank's unpack
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         ev[0].record()
+        K = shards[0].npieces  # (pieces until half the nodes have converged, one after)
+        pieces_per_round.append(K)
         if K == 1:
             for e in shards:
                 e.round()
@@ -126,7 +129,8 @@ summary = {
     "tail_over_dense": phase(per_round, tail_r) / phase(per_round, dense_r) if dense_r and tail_r else None,
     # per rank-round (all ranks / world): round kernels and passes, the copies left exposed after
     # the last piece (in pieces; else all of them), the unpack
-    "pieces": K,
+    "pieces_first": pieces_per_round[0] if pieces_per_round else None,
+    "rounds_in_pieces": sum(1 for k in pieces_per_round if k > 1),
     "compute_ms_dense": phase(compute, dense_r, a.world), "exposed_copies_ms_dense": phase(copies, dense_r, a.world),
     "unpack_ms_dense": phase(unpack, dense_r, a.world),
     "compute_ms_tail": phase(compute, tail_r, a.world), "exposed_copies_ms_tail": phase(copies, tail_r, a.world),
@@ -147,6 +151,7 @@ if a.series:
         json.dump(dict(summary, per_round_ms=[round(x, 4) for x in per_round],
                        compute_ms=[round(x, 4) for x in compute], copies_ms=[round(x, 4) for x in copies],
                        unpack_ms=[round(x, 4) for x in unpack],
-                       send_bytes=send_bytes, round_bytes=round_bytes, trace=trace), f)
+                       send_bytes=send_bytes, round_bytes=round_bytes, trace=trace,
+                       pieces_per_round=pieces_per_round, warmup_pieces=warmup_pieces), f)
 for e in shards:
     e.close()
