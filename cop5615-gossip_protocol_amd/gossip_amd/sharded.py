@@ -106,6 +106,8 @@ class HipShard:
             self._sbp = self._sb.ctypes.data_as(C.c_void_p)
             self._rbp = self._rb.ctypes.data_as(C.c_void_p)
             self._obp = self._ob.ctypes.data_as(C.c_void_p)
+        # pieces until half the nodes have converged, one piece after (the library decides at a sync)
+        self.npieces = int(self.lib.gp_shard_pieces(self.h))
         if self.npieces == 1:
             _abi.check(self.lib.gp_shard_plan(self.h, self._sbp, self._rbp))
             self.send_splits, self.recv_splits = self._sb.tolist(), self._rb.tolist()
