@@ -14,8 +14,11 @@
 #define GP_ACT_PCT 99
 #endif
 constexpr uint32_t kQuietMinActors = 1u << 20;
-// Shards run their rounds in pieces from this many actors on every rank (GP_FLAG_PIECES).
-constexpr int64_t kPieceMinActors = 1 << 20;
+// Shards run their rounds in pieces from this many actors on every rank (GP_FLAG_PIECES):
+// a piece's launches cost a few microseconds each, which 12.5M-actor ranks (100M / 8) do not earn back
+// (dense rank-round 0.43 -> 0.68 ms in pieces) and 125M-actor ranks (C5 / 8) do (+2.6% of kernel time
+// for an exchange of 326 MB per rank-round hidden but for its last piece).
+constexpr int64_t kPieceMinActors = 1 << 25;
 // Full gossip done bitmap: one bit per actor, then its summary (one bit per 32-actor word).
 constexpr uint32_t kDsumMinActors = 1u << 25;  // the summary is used from here (dbits > an L2)
 // Full gossip on one GPU: the receipt tally (gp_kernels.h GsTally) is built from this many actors
@@ -1760,7 +1763,7 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
     g.dy = make_fastdiv(g.gy);
     if (h->world > 1 && !h->full) h->halo = g.gz > 1 ? g.plane : 1u;  // grid rows crossing a shard face
     // A round in pieces: push-sum pull shards whose host exchanges piece by piece
-    // (GP_FLAG_PIECES), from 2^20 actors on every rank (GP_FLAG_FORCE_PIECES: any size), in whole
+    // (GP_FLAG_PIECES), from 2^25 actors on every rank (GP_FLAG_FORCE_PIECES: any size), in whole
     // z-planes (line / 2D: 256 actors), so that the faces stay in the first and the last piece.
     // The same decision on every rank: it depends on the partition only.
     if (sharded && h->world > 1 && !h->gossip && !h->generic && (cfg->flags & GP_FLAG_PIECES)) {

@@ -53,7 +53,8 @@ class HipShard:
         for shards of 2^20 actors or more).  full_plan: no activity tiers (every round ships the
         all-sending capacity); tight_tiers: tiers with no headroom and frequent replays (a test
         hook).  pieces: exchange a push-sum round piece by piece (the library picks 4 pieces from
-        2^20 actors per rank, else 1); force_pieces: 4 pieces at any size (a test hook)."""
+        2^25 actors per rank until half the nodes have converged, else 1); force_pieces: 4 pieces
+        at any size (a test hook)."""
         import torch
 
         if topology not in _abi.TOPOLOGIES:
@@ -251,18 +252,32 @@ def _offsets(splits):
 class LoopbackTransport:
     """All shards live in this process (one GPU, or CPU): chunk p->q is copied from p's send
     buffer into q's receive buffer (stream-ordered device copies for HipShard).  In pieces the
-    copies of piece i run on a stream of their own, after every shard's piece i, while the shards
-    compute piece i+1 (join: the engines' stream waits for the copies)."""
+    copies of piece i run on a stream of their own, after every shard's piece i (piece_done), while
+    the shards compute piece i+1 (join: the engines' stream waits for the copies).  The host issues
+    piece i's copies after piece i+1's kernels (run_local): one process issues every rank's copies,
+    and issued first they kept the kernels of piece i+1 waiting for the host."""
 
     def __init__(self):
         self.stream = None
+        self.done = {}
+
+    def piece_done(self, i):
+        """Every shard's piece i is enqueued on the current stream."""
+        import torch
+
+        self.done[i] = torch.cuda.Event()
+        self.done[i].record()
 
     def exchange_piece_all(self, engines, i):
         import torch
 
         if self.stream is None:
             self.stream = torch.cuda.Stream()
-        self.stream.wait_stream(torch.cuda.current_stream())  # after every shard's piece i
+        ev = self.done.pop(i, None)
+        if ev is not None:
+            self.stream.wait_event(ev)  # after every shard's piece i
+        else:
+            self.stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.stream):
             plans = [e.piece_plans[i] for e in engines]
             so = [_offsets(pl[0]) + pl[2] for pl in plans]
@@ -409,7 +424,10 @@ def run_local(engines, max_rounds: int = 1 << 40, batch: int = 8, max_batch: int
                 for i in range(pieces):
                     for e in engines:
                         e.round_piece(i)
-                    t.exchange_piece_all(engines, i)
+                    t.piece_done(i)
+                    if i:
+                        t.exchange_piece_all(engines, i - 1)
+                t.exchange_piece_all(engines, pieces - 1)
                 t.join()
             for e in engines:
                 e.deliver()

@@ -68,8 +68,9 @@ enum gp_flags {
     GP_FLAG_PIECES = 1024,     /* push-sum shards: the host exchanges each round piece by piece
                                   (gp_shard_round_piece / gp_shard_plan_piece), so the exchange of
                                   one piece overlaps the next piece's kernels; the library runs 4
-                                  pieces when every rank holds 2^20 actors or more, else 1
-                                  (gp_shard_pieces) */
+                                  pieces when every rank holds 2^25 actors or more, until half the
+                                  nodes have converged, else 1 (gp_shard_pieces, re-read after
+                                  every gp_shard_sync) */
     GP_FLAG_FORCE_PIECES = 2048, /* with GP_FLAG_PIECES: 4 pieces at any size (whole z-planes, or
                                   256 actors on line / 2D, permitting); a test hook, same results */
 };

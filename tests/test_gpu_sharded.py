@@ -383,11 +383,14 @@ def test_group_pieces_vs_oracle():
 
 
 def test_shards_imp3d_10m_two_ranks():
-    """BASELINE config 3 split over 2 shards (in 4 pieces each: 5M actors per rank): the same run as
-    the single-GPU engine."""
+    """BASELINE config 3 split over 2 shards (in 4 pieces each, forced: the library runs 5M-actor ranks
+    in one piece): the same run as the single-GPU engine."""
     ref = Simulator(10_000_000, "Imp3D", "push-sum", seed=1)
     rs = ref.step()
-    engines = _shards(10_000_000, "Imp3D", "push-sum", 2, seed=1)
+    one = sharded.HipShard(10_000_000, "Imp3D", "push-sum", rank=0, world=2, seed=1)
+    assert one.npieces == 1  # below 2^25 actors per rank
+    one.close()
+    engines = _shards(10_000_000, "Imp3D", "push-sum", 2, seed=1, force_pieces=True)
     assert all(e.npieces == 4 for e in engines)
     sts = sharded.run_local(engines)
     assert rs.converged and (sts[0].round, sts[0].completed) == (rs.round, rs.completed)

@@ -29,6 +29,7 @@ ap.add_argument("--rounds", type=int, default=None, help="default: to convergenc
 ap.add_argument("--seed", type=int, default=1)
 ap.add_argument("--series", default=None, help="write the per-round series (JSON) here")
 ap.add_argument("--no-pieces", action="store_true", help="one piece per round (no exchange overlap)")
+ap.add_argument("--force-pieces", action="store_true", help="4 pieces at any size (the library's test hook)")
 a = ap.parse_args()
 
 import torch  # noqa: E402
@@ -37,7 +38,7 @@ from gossip_amd import sharded  # noqa: E402
 
 torch.cuda.set_device(0)
 shards = [sharded.HipShard(a.n, a.topology, a.algorithm, rank=r, world=a.world, seed=a.seed, kernel_timing=True,
-                           pieces=not a.no_pieces) for r in range(a.world)]
+                           pieces=not a.no_pieces, force_pieces=a.force_pieces) for r in range(a.world)]
 pieces_per_round = []
 warmup_pieces = shards[0].npieces
 nodes = shards[0].nodes
@@ -60,28 +61,35 @@ while not sts[0].converged and sts[0].round < cap:
         # the whole round on the shards' stream: every rank's round kernels and passes (in pieces:
         # each piece's chunk copies on the transport's own stream, overlapping the next piece), what
         # is left of the copies after the last piece (joined), every rank's unpack
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
         ev[0].record()
         K = shards[0].npieces  # (pieces until half the nodes have converged, one after)
         pieces_per_round.append(K)
-        if K == 1:
-            for e in shards:
+        if K == 1:  # (ev[4], ev[5]: rank 0's own round and unpack, as round 4 measured them)
+            for i, e in enumerate(shards):
                 e.round()
+                if i == 0:
+                    ev[4].record()
             ev[1].record()
             t.exchange_all(shards)
         else:
-            for i in range(K):
+            for i in range(K):  # (piece i's copies issued after piece i+1's kernels: sharded.run_local)
                 for e in shards:
                     e.round_piece(i)
-                t.exchange_piece_all(shards, i)
+                t.piece_done(i)
+                if i:
+                    t.exchange_piece_all(shards, i - 1)
             ev[1].record()
+            t.exchange_piece_all(shards, K - 1)
             t.join()
         round_bytes.append(shards[0].bytes_per_round()[0])  # rank 0's chunks of this round
         ev[2].record()
-        for e in shards:
+        for i, e in enumerate(shards):
             e.deliver()
+            if i == 0 and K == 1:
+                ev[5].record()
         ev[3].record()
-        events.append(ev)
+        events.append((ev, K))
     before = int(sts[0].completed)
     sts = [e.sync() for e in shards]
     assert len({(int(s.round), int(s.completed), int(s.converged)) for s in sts}) == 1, "shards disagree"
@@ -94,12 +102,16 @@ trace = [int(x) for x in shards[0].read_trace()]
 # gossip's F(k) applies round k - 1: one launch more than rounds
 launches = rounds + (1 if a.algorithm == "gossip" else 0)
 nl = min(launches, len(events))
-per_round = [events[i][0].elapsed_time(events[i][3]) for i in range(nl)]
+per_round = [events[i][0][0].elapsed_time(events[i][0][3]) for i in range(nl)]
 # the phases of a round on the shards' stream (all ranks): the round kernels and passes (in pieces
 # the copies of all but the last piece run beside them), the copies not hidden, the unpacks
-compute = [events[i][0].elapsed_time(events[i][1]) for i in range(nl)]
-copies = [events[i][1].elapsed_time(events[i][2]) for i in range(nl)]
-unpack = [events[i][2].elapsed_time(events[i][3]) for i in range(nl)]
+compute = [events[i][0][0].elapsed_time(events[i][0][1]) for i in range(nl)]
+copies = [events[i][0][1].elapsed_time(events[i][0][2]) for i in range(nl)]
+unpack = [events[i][0][2].elapsed_time(events[i][0][3]) for i in range(nl)]
+# rank 0's own work (its round kernels + passes, its unpack; one-piece rounds only): what one GPU of
+# a real node would spend beside its all-to-all
+rank0 = [(events[i][0][0].elapsed_time(events[i][0][4]) + events[i][0][2].elapsed_time(events[i][0][5]))
+         if events[i][1] == 1 else None for i in range(nl)]
 ks = shards[0].kernel_stats()
 
 
@@ -115,7 +127,8 @@ tail_r = [r for r in range(nl) if r < len(prev) and prev[r] * 100 >= 99 * nodes]
 
 
 def phase(xs, rs, div=1.0):
-    return mean([xs[r] for r in rs]) / div if rs else None
+    v = [xs[r] for r in rs if xs[r] is not None]
+    return mean(v) / div if v else None
 
 
 summary = {
@@ -135,6 +148,10 @@ summary = {
     "unpack_ms_dense": phase(unpack, dense_r, a.world),
     "compute_ms_tail": phase(compute, tail_r, a.world), "exposed_copies_ms_tail": phase(copies, tail_r, a.world),
     "unpack_ms_tail": phase(unpack, tail_r, a.world),
+    # rank 0's own round + unpack by hipEvents (one-piece rounds)
+    "rank0_ms_dense": phase(rank0, dense_r), "rank0_ms_tail": phase(rank0, tail_r),
+    "rank0_tail_over_dense": (phase(rank0, tail_r) / phase(rank0, dense_r)
+                              if phase(rank0, dense_r) and phase(rank0, tail_r) else None),
     "rank0_kernel": ks["kernel"], "rank0_kernel_avg_ms": ks["avg_ms"], "rank0_aux": ks["aux_kernel"],
     "rank0_aux_avg_ms": ks["aux_avg_ms"], "rank0_work_per_launch": ks["work_per_launch"],
     "rank0_actors": shards[0].hi - shards[0].lo,
@@ -150,6 +167,7 @@ if a.series:
     with open(a.series, "w") as f:
         json.dump(dict(summary, per_round_ms=[round(x, 4) for x in per_round],
                        compute_ms=[round(x, 4) for x in compute], copies_ms=[round(x, 4) for x in copies],
+                       rank0_ms=[None if x is None else round(x, 4) for x in rank0],
                        unpack_ms=[round(x, 4) for x in unpack],
                        send_bytes=send_bytes, round_bytes=round_bytes, trace=trace,
                        pieces_per_round=pieces_per_round, warmup_pieces=warmup_pieces), f)
