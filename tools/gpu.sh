@@ -15,6 +15,7 @@
 #   ktrun_bench  kernel trace of bench.py with the arguments given as the second argument
 #   pmcrun  FETCH_SIZE and WRITE_SIZE passes over a whole run (prof_run.py, $ROUNDS default: to
 #           convergence) -> tools/pmc_run_summary.py ($PMC_WORKLOAD, $PMC_KERNEL) into $O
+#   pmcphase counters per kernel by phase of one run (tools/pmc_phase_table.py; $PMC_* below the case)
 #   pmcgroup the same passes, summed over the kernels of one round ($PMC_KERNELS, comma list) and
 #           divided by $PMC_ROUNDS -> tools/pmc_group_summary.py ($PMC_WORKLOAD, $PMC_GROUP)
 # Extra prof_run.py arguments: $PROF_ARGS; rounds: $ROUNDS; bench.py arguments: $BENCH_ARGS;
@@ -95,6 +96,19 @@ case $MODE in
     kt kt python3 "$R/bench.py" $2 ;;
   ktrun)  # kernel trace of one prof_run.py run ($ROUNDS rounds, default: to convergence)
     kt kt python3 "$R/tools/prof_run.py" --rounds ${ROUNDS:-1000000} ${PROF_ARGS} ;;
+  pmcphase)  # counters per kernel by phase of one run: one rocprofv3 --pmc run per pass of $PMC_PASSES
+    # (";"-separated counter lists) over "python3 $PMC_CMD --series ..." -> tools/pmc_phase_table.py
+    # ($PMC_RK round kernel, $PMC_WORLD, $PMC_WARMUP rounds before the run, $PMC_KERNELS comma list)
+    IFS=';' read -ra PS <<< "$PMC_PASSES"
+    i=0
+    for c in "${PS[@]}"; do
+      i=$((i+1))
+      ser=""; [ $i -eq 1 ] && ser="--series $O/series.json"
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL ${PMC_TIMEOUT:-150} rocprofv3 --pmc $c --output-format csv -d "$O/pmc_$i" -o p -- python3 $R/$PMC_CMD $ser > "$O/pmc_$i.log" 2>&1 )
+      rc=$?; echo "pmc pass $i ($c) rc=$rc"; tail -1 "$O/pmc_$i.log"; [ $rc -eq 0 ] || exit $rc
+    done
+    python3 "$R/tools/pmc_phase_table.py" "$O/series.json" "$PMC_RK" "${PMC_WORLD:-1}" "${PMC_WARMUP:-0}" "$PMC_KERNELS" "$O/table.md" $(for j in $(seq $i); do echo "$O/pmc_$j"; done) > /dev/null && cat "$O/table.md" | head -${PMC_LINES:-40}
+    [ "${PMC_DROP:-1}" = 1 ] && for j in $(seq $i); do find "$O/pmc_$j" -name '*counter_collection.csv' -size +20M -delete; done ;;
   loopab)
     for v in ${VARIANTS}; do
       GP_LIB=lib_$v kt "kt_$v" python3 "$R/tools/shard_loopback_prof.py" ${LOOP_ARGS} || exit $?

@@ -30,6 +30,10 @@ ap.add_argument("--seed", type=int, default=1)
 ap.add_argument("--series", default=None, help="write the per-round series (JSON) here")
 ap.add_argument("--no-pieces", action="store_true", help="one piece per round (no exchange overlap)")
 ap.add_argument("--force-pieces", action="store_true", help="4 pieces at any size (the library's test hook)")
+ap.add_argument("--spin-us", type=float, default=0.0,
+                help="a GPU spin of this many microseconds before every round, outside the timed events: "
+                     "one host issues all W ranks' launches and copies here, and without a lead the GPU "
+                     "waits for it in the short tail rounds (a node's host issues one rank's, batches ahead)")
 a = ap.parse_args()
 
 import torch  # noqa: E402
@@ -55,6 +59,16 @@ send_bytes = [(0, shards[0].bytes_per_round()[0])]
 round_bytes = []  # rank 0's send bytes per round (full gossip plans every round)
 max_batch = sharded._max_batch(shards[0], 64)
 batch = min(8, max_batch)
+spin_cycles = 0
+if a.spin_us > 0:  # calibrate torch.cuda._sleep's cycles against hipEvents
+    c0 = 1 << 20
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(c0)
+    e0.record()
+    torch.cuda._sleep(c0)
+    e1.record()
+    e1.synchronize()
+    spin_cycles = int(c0 * a.spin_us / (e0.elapsed_time(e1) * 1e3))
 t0 = time.perf_counter()
 while not sts[0].converged and sts[0].round < cap:
     for _ in range(min(batch, cap - int(sts[0].round))):
@@ -62,6 +76,8 @@ while not sts[0].converged and sts[0].round < cap:
         # each piece's chunk copies on the transport's own stream, overlapping the next piece), what
         # is left of the copies after the last piece (joined), every rank's unpack
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        if spin_cycles:
+            torch.cuda._sleep(spin_cycles)
         ev[0].record()
         K = shards[0].npieces  # (pieces until half the nodes have converged, one after)
         pieces_per_round.append(K)
@@ -149,6 +165,7 @@ summary = {
     "compute_ms_tail": phase(compute, tail_r, a.world), "exposed_copies_ms_tail": phase(copies, tail_r, a.world),
     "unpack_ms_tail": phase(unpack, tail_r, a.world),
     # rank 0's own round + unpack by hipEvents (one-piece rounds)
+    "spin_us": a.spin_us,
     "rank0_ms_dense": phase(rank0, dense_r), "rank0_ms_tail": phase(rank0, tail_r),
     "rank0_tail_over_dense": (phase(rank0, tail_r) / phase(rank0, dense_r)
                               if phase(rank0, dense_r) and phase(rank0, tail_r) else None),
