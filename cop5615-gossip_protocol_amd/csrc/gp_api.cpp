@@ -1246,6 +1246,14 @@ Xchg make_xchg(const Handle* h, void* send, const void* recv, int i = 0) {
 // Index of the round F(k) applies (its completion count), -1 for gossip's emit-only F(0).
 long long applied_round(const Handle* h, int64_t k) { return h->gossip ? (long long)k - 1 : (long long)k; }
 
+// A push-sum shard's tail round writes its halo faces in its round kernel (k_ps_quiet_x<true>,
+// DESIGN.md §6.12): the rounds that are certainly tail rounds, by the rule that drops the link
+// scatter (launch_aux), with links (the kernel that walks them) and one piece.
+bool halo_inline(const Handle* h, int64_t k) {
+    return !h->gossip && !h->generic && h->g.has_link && h->halo && h->npiece == 1 && h->act[0] && h->act_thr &&
+           h->completed >= (int64_t)h->act_thr && k >= h->rounds + 1;
+}
+
 // Piece `piece` of round k: its round kernel and link pass, the halo face it holds, its headers.  The
 // pieces of a round are packed in order; the last one completes the round (gp_shard_deliver next).
 int shard_round_piece(Handle* h, void* send, int piece) {
@@ -1268,12 +1276,13 @@ int shard_round_piece(Handle* h, void* send, int piece) {
             h->round_slot = h->timed_count++;
         }
     }
-    const Xchg x = make_xchg(h, send, nullptr, piece);
+    Xchg x = make_xchg(h, send, nullptr, piece);
+    x.hin = halo_inline(h, k) ? 1u : 0u;
     if ((rc = launch_round(h, k, &x, h->round_slot >= 0, std::max<int64_t>(h->round_slot, 0), piece))) return rc;
     const RoundArgs a = h->args((uint32_t)k);
     // the halo face this piece holds (the rank's first actors to rank-1, its last to rank+1), then the
     // headers
-    launch_shard_halo(a, x, h->gossip ? 0 : 1, h->stream);
+    if (!x.hin) launch_shard_halo(a, x, h->gossip ? 0 : 1, h->stream);
     launch_shard_pack(a, x, applied_round(h, k), h->stream);
     HIP_TRY(hipGetLastError());
     for (int q = 0; q < h->world; ++q) h->bytes_sent += (int64_t)h->out_chunk[(size_t)piece * h->world + q].size;

@@ -194,6 +194,8 @@ struct Xchg {
     uint32_t world, rank;
     uint32_t last;                 // the round's last piece: its headers carry the
                                    // round's count (pack), its unpack publishes total[applied]
+    uint32_t hin;                  // push-sum tail round: the round kernel writes the halo faces
+                                   // (k_ps_quiet_x<true>; k_shard_halo is not launched)
     uint32_t abnd[kMaxWorld + 1];  // actor range of every rank
     uint32_t sbnd[kMaxWorld + 1];  // link-slot range of every rank (global CSR numbering)
     uint32_t* pcount;              // entry counters of the current round, (peer, sub) then (world +

@@ -388,12 +388,15 @@ __device__ __forceinline__ PsLevel1 ps_level1(const RoundArgs& a, const Geom& g,
 // kernel, which spills with one load per unrolled slot) instead of one per unrolled slot.
 // A shard's quiet-tail round routes its own link messages (the scatter pass's work in the dense
 // rounds): ps_finish reports the message of an actor whose round-r message took its extra link.
+// HD (a shard's tail round that writes its own halo faces, k_ps_quiet_x<true>): also every send's
+// direction code and message.
 struct LinkSend {
     bool fired = false;
     double2 msg;
+    uint32_t dir = kDirNone;
 };
 
-template <int LM, bool PRE = false, bool FF = (LM == 1)>
+template <int LM, bool PRE = false, bool FF = (LM == 1), bool HD = false>
 __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
                                               const PsLevel1& p, bool mark, LinkSend* ls = nullptr) {
     const uint32_t m = p.m;
@@ -577,7 +580,11 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
             a.lcnt_cur[lp] = (uint8_t)a.tag_cur;
         }
     }
-    if (LM == 2 && ls && o.send && code == kDirLink) {
+    if constexpr (LM == 2 && HD) {
+        ls->dir = o.send ? code : kDirNone;
+        ls->fired = o.send && code == kDirLink;
+        ls->msg = o.msg;
+    } else if (LM == 2 && ls && o.send && code == kDirLink) {
         ls->fired = true;
         ls->msg = o.msg;
     }
@@ -598,10 +605,10 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
     return o.conv_now ? 1u : 0u;
 }
 
-template <int LM, bool FF = (LM == 1)>
+template <int LM, bool FF = (LM == 1), bool HD = false>
 __device__ __forceinline__ uint32_t ps_actor(const RoundArgs& a, const Geom& g, uint32_t r, uint32_t v,
                                              bool mark = false, LinkSend* ls = nullptr) {
-    return ps_finish<LM, false, FF>(a, g, r, v, ps_level1<LM>(a, g, r, v), mark, ls);
+    return ps_finish<LM, false, FF, HD>(a, g, r, v, ps_level1<LM>(a, g, r, v), mark, ls);
 }
 
 // The quiet-wave tail with compaction.  Marks are per segment of kActSeg actors: F(r) marks the
@@ -657,7 +664,11 @@ __device__ __forceinline__ TailWalk tail_walk(const RoundArgs& a, bool tail) {
 // segments is listed (or the span ends), so a pass of the late tail, where a chunk holds one or
 // two marked segments, keeps its 64 lanes busy (one pass per chunk left 1-2 segments per pass);
 // each chunk's unmarked segments get "send nothing" (kDirNone) direction bytes as it is opened.
-__device__ __forceinline__ bool tail_next(const RoundArgs& a, TailWalk& t, uint8_t tag, uint32_t& v) {
+// HIN (a shard's tail round that writes its own halo faces): those of face actors into the chunks
+// of rank -+ 1 too.
+template <bool HIN = false>
+__device__ __forceinline__ bool tail_next(const RoundArgs& a, TailWalk& t, uint8_t tag, uint32_t& v,
+                                          const Xchg* hx = nullptr) {
     constexpr uint32_t S = kActSeg, PER = 64u / kActSeg;
     const uint32_t lane = threadIdx.x & 63u;
     while (t.c - t.k < PER && t.base < t.s1) {
@@ -686,6 +697,17 @@ __device__ __forceinline__ bool tail_next(const RoundArgs& a, TailWalk& t, uint8
 #pragma unroll
                 for (uint32_t i = 0; i < S; ++i) __builtin_nontemporal_store(kDirNone, d + i);
             }
+            if constexpr (HIN) {
+#pragma unroll
+                for (uint32_t sd = 0; sd < 2; ++sd) {
+                    const uint32_t f0 = hx->h.out_first[sd], n = hx->h.out_n[sd], b = seg * S;
+                    if (b + S > f0 && b < f0 + n) {  // (a face is whole planes: rarely astride a segment)
+#pragma unroll
+                        for (uint32_t i = 0; i < S; ++i)
+                            if (b + i - f0 < n) hx->h.out_dir[sd][b + i - f0] = kDirNone;
+                    }
+                }
+            }
         }
         const uint64_t m = __ballot(act);
         if (act) t.list[t.c + mbcnt64(m)] = seg;
@@ -706,7 +728,10 @@ __device__ __forceinline__ bool tail_next(const RoundArgs& a, TailWalk& t, uint8
 // did not mark has only converged actors and receives nothing, so its round is "send nothing":
 // its direction bytes become kDirNone and nothing else changes.
 // Q: quiet-wave marks allocated (a.act_cur != null); the small graphs run without (Q = false).
-template <int LM, bool Q>
+// HIN (LM 2, tail rounds only: the host knows from the synced count): the walk writes the halo faces
+// itself, the direction byte of every face actor and the messages that cross, so k_shard_halo is not
+// launched.
+template <int LM, bool Q, bool HIN = false>
 __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp = nullptr) {
     const Geom g = a.g;
     const uint32_t r = a.r;
@@ -748,7 +773,7 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
         for (;;) {
             uint32_t u;
             if (tail) {
-                if (!tail_next(a, t, tag, u)) break;
+                if (!tail_next<HIN>(a, t, tag, u, xp)) break;
             } else {
                 if (v >= end) break;
                 u = v;
@@ -756,7 +781,7 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
             }
             LinkSend ls;
             if (u - a.lo < a.hi - a.lo) {  // lo <= u < hi (a shard's edge segments)
-                newly += ps_actor<LM, LM == 1 || LM == 2>(a, g, r, u, mark, LM == 2 ? &ls : nullptr);
+                newly += ps_actor<LM, LM == 1 || LM == 2, HIN>(a, g, r, u, mark, LM == 2 ? &ls : nullptr);
                 ++walked;
             }
             if constexpr (LM == 2) {
@@ -771,6 +796,27 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
                     const uint32_t q = remote ? owner(x.sbnd, x.world, lp) : 0u;
                     const uint32_t pos = wave_reserve(x, remote, q);
                     if (remote) put<true>(x, q, pos, lp, ls.msg);
+                }
+            }
+            if constexpr (LM == 2 && HIN) {  // the halo faces (k_shard_halo's work; wave-uniform here)
+                const Xchg& x = *xp;
+                const bool own = u - a.lo < a.hi - a.lo;
+#pragma unroll
+                for (uint32_t sd = 0; sd < 2; ++sd) {
+                    const uint32_t fo = u - x.h.out_first[sd];
+                    const bool face = own && fo < x.h.out_n[sd];
+                    if (face) x.h.out_dir[sd][fo] = (uint8_t)ls.dir;
+                    const bool cross = face && ls.dir == x.h.code[sd];
+                    const uint32_t pos = wave_reserve(x, cross, x.world + sd);
+                    if (cross) {
+                        const uint32_t cap = x.h.out_cap[sd];
+                        if (pos < cap) {
+                            x.h.out_slot[sd][my_sub() * cap + pos] = fo;
+                            x.h.out_msg[sd][my_sub() * cap + pos] = ls.msg;
+                        } else {
+                            atomicOr(x.overflow, 1u);
+                        }
+                    }
                 }
             }
         }
@@ -798,10 +844,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PSQ_W
     ps_pull_body<LM, true>(a);
 }
 // A shard of several ranks (LM 2): the same kernel with the exchange descriptor, so its tail rounds
-// route their own link messages.
+// route their own link messages (HIN: and write the halo faces).
+template <bool HIN>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PSQ_WAVES))) GP_PSQ_SGPR_ATTR void k_ps_quiet_x(
     RoundArgs a, Xchg x) {
-    ps_pull_body<2, true>(a, &x);
+    ps_pull_body<2, true, HIN>(a, &x);
 }
 
 // ------------------------------------------------------------------ gossip, grid topologies
@@ -2404,7 +2451,8 @@ void launch_ps_pull(const RoundArgs& a, const Launch& l, const Xchg* x) {
     } else if (a.rmsg_prev && !a.sharded) {  // one GPU, small graph: link messages by slot
         hipLaunchKernelGGL((k_ps_pull<3, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
     } else if (a.rmsg_prev) {  // a shard of several ranks
-        if (q) hipLaunchKernelGGL(k_ps_quiet_x, dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a, *x);
+        if (q && x->hin) hipLaunchKernelGGL(k_ps_quiet_x<true>, dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a, *x);
+        else if (q) hipLaunchKernelGGL(k_ps_quiet_x<false>, dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a, *x);
         else hipLaunchKernelGGL((k_ps_pull<2, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
     } else if (q) {
         hipLaunchKernelGGL((k_ps_quiet<1>), dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a);

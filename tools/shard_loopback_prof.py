@@ -30,6 +30,9 @@ ap.add_argument("--seed", type=int, default=1)
 ap.add_argument("--series", default=None, help="write the per-round series (JSON) here")
 ap.add_argument("--no-pieces", action="store_true", help="one piece per round (no exchange overlap)")
 ap.add_argument("--force-pieces", action="store_true", help="4 pieces at any size (the library's test hook)")
+ap.add_argument("--rank0-events", action="store_true",
+                help="also bracket rank 0's own round and unpack with events (each record stalls the queue "
+                     "for a few microseconds, inside the phases the other figures time)")
 ap.add_argument("--spin-us", type=float, default=0.0,
                 help="a GPU spin of this many microseconds before every round, outside the timed events: "
                      "one host issues all W ranks' launches and copies here, and without a lead the GPU "
@@ -81,10 +84,11 @@ while not sts[0].converged and sts[0].round < cap:
         ev[0].record()
         K = shards[0].npieces  # (pieces until half the nodes have converged, one after)
         pieces_per_round.append(K)
-        if K == 1:  # (ev[4], ev[5]: rank 0's own round and unpack, as round 4 measured them)
+        r0 = a.rank0_events and K == 1  # (ev[4], ev[5]: rank 0's own round and unpack, as round 4 timed them)
+        if K == 1:
             for i, e in enumerate(shards):
                 e.round()
-                if i == 0:
+                if i == 0 and r0:
                     ev[4].record()
             ev[1].record()
             t.exchange_all(shards)
@@ -102,10 +106,10 @@ while not sts[0].converged and sts[0].round < cap:
         ev[2].record()
         for i, e in enumerate(shards):
             e.deliver()
-            if i == 0 and K == 1:
+            if i == 0 and r0:
                 ev[5].record()
         ev[3].record()
-        events.append((ev, K))
+        events.append((ev, K if r0 or K > 1 else 0))
     before = int(sts[0].completed)
     sts = [e.sync() for e in shards]
     assert len({(int(s.round), int(s.completed), int(s.converged)) for s in sts}) == 1, "shards disagree"
@@ -128,6 +132,8 @@ unpack = [events[i][0][2].elapsed_time(events[i][0][3]) for i in range(nl)]
 # a real node would spend beside its all-to-all
 rank0 = [(events[i][0][0].elapsed_time(events[i][0][4]) + events[i][0][2].elapsed_time(events[i][0][5]))
          if events[i][1] == 1 else None for i in range(nl)]
+# every rank's round kernels and unpacks without the copies, per rank (hipEvents around whole phases)
+kern = [compute[i] + unpack[i] for i in range(nl)]
 ks = shards[0].kernel_stats()
 
 
@@ -156,6 +162,8 @@ summary = {
     "rank_round_ms_dense": phase(per_round, dense_r, a.world),
     "rank_round_ms_tail": phase(per_round, tail_r, a.world),
     "tail_over_dense": phase(per_round, tail_r) / phase(per_round, dense_r) if dense_r and tail_r else None,
+    "kernels_ms_dense": phase(kern, dense_r, a.world), "kernels_ms_tail": phase(kern, tail_r, a.world),
+    "kernels_tail_over_dense": phase(kern, tail_r) / phase(kern, dense_r) if dense_r and tail_r else None,
     # per rank-round (all ranks / world): round kernels and passes, the copies left exposed after
     # the last piece (in pieces; else all of them), the unpack
     "pieces_first": pieces_per_round[0] if pieces_per_round else None,
