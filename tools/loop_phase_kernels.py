@@ -34,7 +34,7 @@ def main():
     per = defaultdict(lambda: defaultdict(float))  # round -> kernel -> us (all ranks)
     for r in rows:
         n = name(r)
-        if n == rk:
+        if n == rk or n.startswith(rk + "<"):  # (k_ps_quiet_x<false> / <true>)
             if seen < acc:
                 rnd = bisect.bisect_right(starts, seen) - 1 - 8
             else:  # launched past the recorded rounds (one piece each)

@@ -41,7 +41,7 @@ def rounds_of(disp, rk, world, warmup):
     seen, rnd, out = 0, -1, {}
     for did in sorted(disp):
         k = disp[did][0]
-        if k == rk:
+        if k == rk or k.startswith(rk + "<"):  # (k_ps_quiet_x<false> / <true>)
             rnd = seen // world - warmup
             seen += 1
         out[did] = rnd if rnd >= 0 else None
