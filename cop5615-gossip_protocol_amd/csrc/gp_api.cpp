@@ -127,7 +127,9 @@ struct Ckpt {
     double2* msg = nullptr;
     uint8_t* dir = nullptr;
     uint8_t* lcnt = nullptr;
-    double2* rmsg = nullptr;
+    uint32_t* lref = nullptr;  // push-sum shards: the slots' references of round k0-1
+    char* rin = nullptr;       // and the receive buffer they point into (recv_total bytes)
+    bool has_rin = false;
     uint8_t* flags = nullptr;
     uint8_t* act = nullptr;
     unsigned long long* work = nullptr;
@@ -215,7 +217,9 @@ struct Handle {
     uint32_t* rev_src = nullptr;
     uint32_t* lpos = nullptr;
     uint8_t* lcnt[2] = {nullptr, nullptr};   // gossip link slots
-    double2* rmsg[2] = {nullptr, nullptr};   // shards, push-sum: remote senders' link messages per CSR slot
+    double2* rmsg[2] = {nullptr, nullptr};   // small one-GPU graphs: every link message per CSR slot
+    uint32_t* lref[2] = {nullptr, nullptr};  // push-sum shards: slot references (gp_kernels.h kRefShift)
+    const void* msg_src = nullptr;           // the receive buffer the next round reads remote messages from
     uint32_t* slot_dst = nullptr;            // shards with the quiet tail: receiver of each own CSR slot
     // push-sum
     double2* msg[2] = {nullptr, nullptr};
@@ -339,6 +343,11 @@ struct Handle {
         a.msg_cur = msg[c];
         a.rmsg_prev = rmsg[p];
         a.rmsg_cur = rmsg[c];
+        a.lref_prev = lref[p];
+        a.lref_cur = lref[c];
+        a.rtag_prev = r ? ref_tag(r - 1u) : 0u;
+        a.rtag_cur = ref_tag(r);
+        a.rin_prev = static_cast<const double2*>(msg_src);
         a.dir_prev = dir[p];
         a.dir_cur = dir[c];
         a.work = (cfg.flags & GP_FLAG_KERNEL_TIMING) && act[0] ? work : nullptr;
@@ -376,6 +385,10 @@ Xchg base_xchg(const Handle* h);
 // senders target its actors, at which global slot, and the per-peer link counts that size the
 // exchange.  Three transient arrays over all destinations (counts, offsets, the own senders'
 // offsets) live only during the build.
+// A push-sum shard keeps 32-bit slot references; its link pass writes them (a
+// one-rank shard too: the library group at num_gpus = 1).
+bool refs(const Handle* h) { return h->sharded && !h->gossip && !h->generic; }
+
 int build_links(Handle* h) {
     const uint32_t nodes = (uint32_t)h->lay.nodes, A = h->g.actors;
     const uint32_t lo = h->lo, hi = h->hi, shi_src = std::min(hi, nodes);  // own senders [lo, shi_src)
@@ -447,13 +460,17 @@ int build_links(Handle* h) {
     const int64_t nsl = (int64_t)shi - slo;
     if (!h->generic) {  // pull kernels
         // per-slot link marks of the own slots (gossip chains, push-sum round tags)
-        if ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))) return rc;
-        // a remote sender's link message lands in the receiver's slot, read in CSR order (k_ps_pull<2>);
-        // on a small one-GPU graph every link message does (k_ps_pull<3>, the latency-bound rounds)
+        // (a push-sum shard: 32-bit references)
+        if (refs(h)) {
+            if ((rc = h->alloc(&h->lref[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lref[1], (size_t)nsl, slo))) return rc;
+        } else if ((rc = h->alloc(&h->lcnt[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->lcnt[1], (size_t)nsl, slo))) {
+            return rc;
+        }
+        // on a small one-GPU graph every link message lands in the receiver's slot (k_ps_pull<3>, the
+        // latency-bound rounds)
         // (one GPU: up to 2^18 actors; at 1M actors the scattered 16-byte slot stores cost more than
         // the load level they save, profiles/round4/small_imp3d)
-        const bool slot_msgs = (h->sharded && h->world > 1) ||
-                               (!h->sharded && !h->act[0] && h->g.actors < kSlotMsgMaxActors);
+        const bool slot_msgs = !h->sharded && !h->act[0] && h->g.actors < kSlotMsgMaxActors;
         if (slot_msgs && !h->gossip &&
             ((rc = h->alloc(&h->rmsg[0], (size_t)nsl, slo)) || (rc = h->alloc(&h->rmsg[1], (size_t)nsl, slo))))
             return rc;
@@ -547,12 +564,14 @@ int reset(Handle* h) {
         HIP_TRY(hipMemsetAsync(h->pcount, 0, ((size_t)h->world + 2) * kSub * kCtrStride * sizeof(uint32_t), h->stream));
         HIP_TRY(hipMemsetAsync(h->overflow, 0, sizeof(uint32_t), h->stream));
     }
-    if (h->lcnt[0]) {  // no link message in flight
+    if (h->lcnt[0] || h->lref[0]) {  // no link message in flight
         const size_t slo = (size_t)h->sbnd[h->rank], ns = (size_t)(h->sbnd[h->rank + 1] - h->sbnd[h->rank]);
         for (int i = 0; i < 2; ++i) {
             if (h->lcnt[i]) HIP_TRY(hipMemsetAsync(h->lcnt[i] + slo, 0, ns, h->stream));
+            if (h->lref[i]) HIP_TRY(hipMemsetAsync(h->lref[i] + slo, 0, ns * sizeof(uint32_t), h->stream));
         }
     }
+    h->msg_src = nullptr;
     if (!h->gossip) {
         launch_ps_init(h->flags, h->g, h->lo, h->hi, h->full ? 1u : 0u, (uint32_t)h->cfg.term_init, h->L());
         if (h->generic) {
@@ -660,7 +679,7 @@ const char* round_kernel_name(const Handle* h) {
     }
     if (h->gossip) return h->sharded ? "k_gs_full4x" : "k_gs_push";
     if (h->generic) return "k_ps_push_emit";
-    if (h->sharded && h->g.has_link && h->rmsg[0]) return h->act[0] ? "k_ps_quiet_x" : "k_ps_pull<2, false>";
+    if (h->sharded && h->g.has_link && h->lref[0]) return h->act[0] ? "k_ps_quiet_x" : "k_ps_pull<2, false>";
     if (h->g.has_link && h->rmsg[0]) return "k_ps_pull<3, false>";
     if (h->g.has_link) return h->act[0] ? "k_ps_quiet<1>" : "k_ps_pull<1, false>";
     return h->act[0] ? "k_ps_quiet<0>" : "k_ps_pull<0, false>";
@@ -701,9 +720,11 @@ double bytes_per_round(const Handle* h) {
 // repeats in it (link_tag), after F(r-1) has read it and before round r's marks are written
 // (by F(r) itself when the marks are fused, else by the pass after it).
 int clear_tags_if_due(Handle* h, uint32_t r) {
-    if (h->gossip || !h->lcnt[0] || !tag_clear_round(r)) return GP_OK;
-    const int64_t slo = h->sbnd[h->rank], ns = h->sbnd[h->rank + 1] - slo;
-    HIP_TRY(hipMemsetAsync(h->lcnt[r & 1u] + slo, 0, (size_t)ns, h->stream));
+    if (h->gossip) return GP_OK;
+    const int64_t slo = h->sbnd.empty() ? 0 : h->sbnd[h->rank], ns = h->sbnd.empty() ? 0 : h->sbnd[h->rank + 1] - slo;
+    if (h->lcnt[0] && tag_clear_round(r)) HIP_TRY(hipMemsetAsync(h->lcnt[r & 1u] + slo, 0, (size_t)ns, h->stream));
+    if (h->lref[0] && ref_clear_round(r))  // (references: 31 tag values, every 62 rounds)
+        HIP_TRY(hipMemsetAsync(h->lref[r & 1u] + slo, 0, (size_t)ns * sizeof(uint32_t), h->stream));
     return GP_OK;
 }
 
@@ -1156,6 +1177,8 @@ int build_plan(Handle* h) {
     }
     h->send_total = st;
     h->recv_total = rt;
+    if (refs(h) && (uint64_t)rt / 16u >= (1ull << (32 - kRefShift)))
+        return fail(GP_ENOMEM, "a receive buffer of %lld bytes is past the slot references' reach", (long long)rt);
     int rc;
     if ((rc = h->alloc(&h->pcount, ((size_t)W + 2) * kSub * kCtrStride)) || (rc = h->alloc(&h->overflow, 1)) ||
         (rc = h->alloc(&h->self_newly, 1)) || (rc = h->alloc(&h->pmax, (size_t)kMaxPieces * kMaxWorld)))
@@ -1189,6 +1212,7 @@ Xchg make_xchg(const Handle* h, void* send, const void* recv, int i = 0) {
     Xchg x = base_xchg(h);
     const int W = h->world;
     x.last = i == h->npiece - 1 ? 1u : 0u;
+    x.rbase = static_cast<const char*>(recv);
     x.pmax = h->pmax + (size_t)i * kMaxWorld;
     for (int q = 0; q < h->world; ++q) {
         if (q == h->rank) continue;
@@ -1307,6 +1331,10 @@ int shard_deliver(Handle* h, const void* recv) {
     if (!h->awaiting_deliver) return fail(GP_ESTATE, "gp_shard_deliver without gp_shard_round");
     if (!recv && h->recv_total) return fail(GP_EINVAL, "null receive buffer");
     if (reinterpret_cast<uintptr_t>(recv) % kAlign) return fail(GP_EINVAL, "receive buffer not %zu-byte aligned", kAlign);
+    // round k + 1 reads round k's remote messages where they arrived; in pieces the
+    // next round's exchange overlaps that round's kernels, so the host alternates two buffers
+    if (refs(h) && h->npiece > 1 && recv && recv == h->msg_src)
+        return fail(GP_EINVAL, "in pieces consecutive rounds need different receive buffers (the next round reads this one)");
     const int64_t k = h->next_kernel;
     // one kernel per piece applies its halo face (rank-1's last actors land below lo, rank+1's first
     // at hi) and link entries; the last publishes the round's count
@@ -1324,6 +1352,7 @@ int shard_deliver(Handle* h, const void* recv) {
     HIP_TRY(hipGetLastError());
     h->awaiting_deliver = false;
     h->last_recv = recv;
+    if (refs(h)) h->msg_src = recv;
     ++h->delivered;
     h->next_kernel = k + 1;
     if (gossip_plans(h)) gossip_round_plan(h, h->next_kernel);  // full gossip: a plan per round
@@ -1437,7 +1466,9 @@ int ensure_ckpt(Handle* h) {
     const size_t nsl = (size_t)(h->sbnd.empty() ? 0 : h->sbnd[h->rank + 1] - h->sbnd[h->rank]);
     if ((rc = h->alloc(&c.msg, xn)) || (rc = h->alloc(&c.dir, xn)) || (rc = h->alloc(&c.flags, n))) return rc;
     if (h->work && (rc = h->alloc(&c.work, (size_t)kParts * kWorkStride))) return rc;
-    if (h->lcnt[0] && ((rc = h->alloc(&c.lcnt, nsl)) || (rc = h->alloc(&c.rmsg, nsl)))) return rc;
+    if (h->lcnt[0] && (rc = h->alloc(&c.lcnt, nsl))) return rc;
+    if (h->lref[0] && ((rc = h->alloc(&c.lref, nsl)) || (rc = h->alloc(&c.rin, (size_t)std::max<int64_t>(h->recv_total, 1)))))
+        return rc;
     if (h->act[0] && (rc = h->alloc(&c.act, act_bytes(h)))) return rc;
     c.allocated = true;
     return GP_OK;
@@ -1482,9 +1513,20 @@ int ckpt_copy(Handle* h, bool save) {
     if (h->lcnt[0]) {
         const size_t slo = (size_t)h->sbnd[h->rank], nsl = (size_t)(h->sbnd[h->rank + 1] - h->sbnd[h->rank]);
         HIP_TRY(cp(h->lcnt[p] + slo, c.lcnt, nsl));
-        HIP_TRY(cp(h->rmsg[p] + slo, c.rmsg, nsl * sizeof(double2)));
         // the marks of round k0 land in the other array: a failed batch's are cleared
         if (!save) HIP_TRY(hipMemsetAsync(h->lcnt[p ^ 1] + slo, 0, nsl, s));
+    }
+    if (h->lref[0]) {  // the references of round k0-1 and the receive buffer they point into
+        const size_t slo = (size_t)h->sbnd[h->rank], nsl = (size_t)(h->sbnd[h->rank + 1] - h->sbnd[h->rank]);
+        HIP_TRY(cp(h->lref[p] + slo, c.lref, nsl * sizeof(uint32_t)));
+        if (!save) HIP_TRY(hipMemsetAsync(h->lref[p ^ 1] + slo, 0, nsl * sizeof(uint32_t), s));
+        if (save) {
+            c.has_rin = h->msg_src != nullptr;
+            if (c.has_rin && h->msg_src != c.rin)
+                HIP_TRY(hipMemcpyAsync(c.rin, h->msg_src, (size_t)h->recv_total, hipMemcpyDeviceToDevice, s));
+        } else {
+            h->msg_src = c.has_rin ? c.rin : nullptr;  // F(k0) reads round k0-1's messages from the copy
+        }
     }
     if (h->act[0]) HIP_TRY(cp(h->act[k0 & 1] + act_first(h), c.act, act_bytes(h)));
     }
@@ -1992,6 +2034,11 @@ struct Group {
     std::vector<Handle*> shard;
     std::vector<int> dev;
     std::vector<void*> send, recv;
+    // two receive buffers per shard (round parity par): a push-sum round reads the previous round's
+    // remote messages where they arrived
+    std::vector<int64_t> rstride;
+    int par = 0;
+    char* rbuf(int p) const { return static_cast<char*>(recv[(size_t)p]) + par * rstride[(size_t)p]; }
     std::vector<ncclComm_t> comm;
     hipStream_t shared = nullptr;
     // rounds in pieces: the exchange of each piece runs on a stream of its own per
@@ -2045,7 +2092,7 @@ int group_exchange_rccl(Group& G, const Rccl& R, int i, bool split) {
             if (q == p) continue;
             const size_t c = (size_t)i * W + q, ns = s->out_chunk[c].size, nr = s->in_chunk[c].size;
             if (ns) RCCL_TRY(R.send(static_cast<char*>(G.send[p]) + s->out_off[c], ns, ncclUint8, q, G.comm[p], st));
-            if (nr) RCCL_TRY(R.recv(static_cast<char*>(G.recv[p]) + s->in_off[c], nr, ncclUint8, q, G.comm[p], st));
+            if (nr) RCCL_TRY(R.recv(G.rbuf(p) + s->in_off[c], nr, ncclUint8, q, G.comm[p], st));
         }
     }
     return GP_OK;
@@ -2070,7 +2117,7 @@ int group_exchange(Group& G, int i = 0) {
                 const size_t c = (size_t)i * W + q;
                 const int64_t n = (int64_t)G.shard[p]->out_chunk[c].size;
                 if (q == p || !n) continue;
-                HIP_TRY(hipMemcpyAsync(static_cast<char*>(G.recv[q]) + G.shard[q]->in_off[(size_t)i * W + p],
+                HIP_TRY(hipMemcpyAsync(G.rbuf(q) + G.shard[q]->in_off[(size_t)i * W + p],
                                        static_cast<char*>(G.send[p]) + G.shard[p]->out_off[c], (size_t)n,
                                        hipMemcpyDeviceToDevice, st));
             }
@@ -2137,8 +2184,9 @@ int group_step(Handle* h, int64_t max_rounds, gp_status* st) {
             if ((rc = group_exchange_join(G))) return rc;
             for (int p = 0; p < G.W; ++p) {
                 if (!G.one_device) HIP_TRY(hipSetDevice(G.dev[p]));
-                if ((rc = shard_deliver(G.shard[p], G.recv[p]))) return rc;
+                if ((rc = shard_deliver(G.shard[p], G.rbuf(p)))) return rc;
             }
+            G.par ^= 1;
         }
         const int64_t before = G.completed;
         if ((rc = group_sync(G, sts))) return rc;
@@ -2220,6 +2268,7 @@ int group_create(const gp_config* cfg, gp_layout* out, void** handle) {
     G.shard.assign((size_t)W, nullptr);
     G.send.assign((size_t)W, nullptr);
     G.recv.assign((size_t)W, nullptr);
+    G.rstride.assign((size_t)W, 0);
     int64_t bytes = 0;
     for (int p = 0; p < W; ++p) {
         gp_config c = *cfg;
@@ -2240,9 +2289,10 @@ int group_create(const gp_config* cfg, gp_layout* out, void** handle) {
         if ((rc = set_dev(G.dev[p]))) return bail(rc);
         if (s->send_total && hipMalloc(&G.send[p], (size_t)s->send_total) != hipSuccess)
             return bail(fail(GP_ENOMEM, "exchange send buffer of %lld bytes", (long long)s->send_total));
-        if (s->recv_total && hipMalloc(&G.recv[p], (size_t)s->recv_total) != hipSuccess)
-            return bail(fail(GP_ENOMEM, "exchange receive buffer of %lld bytes", (long long)s->recv_total));
-        bytes += lay.device_bytes + s->send_total + s->recv_total;
+        G.rstride[(size_t)p] = (s->recv_total + (int64_t)kAlign - 1) / (int64_t)kAlign * (int64_t)kAlign;
+        if (s->recv_total && hipMalloc(&G.recv[p], (size_t)(2 * G.rstride[(size_t)p])) != hipSuccess)
+            return bail(fail(GP_ENOMEM, "exchange receive buffers of 2 x %lld bytes", (long long)s->recv_total));
+        bytes += lay.device_bytes + s->send_total + 2 * G.rstride[(size_t)p];
         if (p == 0) h->lay = lay;
     }
     if (G.shard[0]->kpiece > 1) {  // the exchange streams and events of the pieces

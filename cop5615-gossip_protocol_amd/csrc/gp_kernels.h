@@ -48,6 +48,13 @@ constexpr bool kFuseLinkMarks = true;
 // (tag_clear_round), so no consumer ever clears a slot and no stale mark can match.
 __host__ __device__ inline uint8_t link_tag(uint32_t r) { return (uint8_t)((r >> 1) % 255u + 1u); }
 __host__ __device__ inline bool tag_clear_round(uint32_t r) { return r >= 2u && (r >> 1) % 255u == 0u; }
+// A push-sum shard's link slots hold 32-bit references instead: the round tag in
+// the low kRefShift bits (ref_tag, 31 values, the same ping-pong rule, cleared every 62 rounds) and,
+// for a remote sender's message, its 16-byte index in the receive buffer of the exchange that
+// delivered it (the pull reads it there).
+constexpr uint32_t kRefShift = 5, kRefTagMask = (1u << kRefShift) - 1u;
+__host__ __device__ inline uint32_t ref_tag(uint32_t r) { return (r >> 1) % kRefTagMask + 1u; }
+__host__ __device__ inline bool ref_clear_round(uint32_t r) { return r >= 2u && (r >> 1) % kRefTagMask == 0u; }
 
 // One synchronous round kernel F(r) fuses phase 2 of round r-1 (collect the messages sent to
 // this actor, read from the round r-1 buffers) with phase 1 of round r (update, convergence
@@ -91,10 +98,16 @@ struct RoundArgs {
     // shard's remote sender's message is written into rmsg by the exchange).
     uint8_t* lcnt_prev;
     uint8_t* lcnt_cur;
+    // push-sum shards: the slots' 32-bit references (kRefShift above), ref_tag(r - 1) / ref_tag(r),
+    // and the receive buffer of round r - 1's exchange (the remote messages F(r) reads, 16 bytes each)
+    const uint32_t* lref_prev;
+    uint32_t* lref_cur;
+    uint32_t rtag_prev, rtag_cur;
+    const double2* rin_prev;
     // push-sum state
     const double2* msg_prev;  // message emitted in round r-1 (= held S,W when not converged)
     double2* msg_cur;
-    // shards (world > 1): link messages of remote senders, by CSR slot (written by the exchange)
+    // small one-GPU graphs (LM 3): every link message by CSR slot
     const double2* rmsg_prev;
     double2* rmsg_cur;
     const uint8_t* dir_prev;  // direction code of that message (kDirNone: none)
@@ -196,6 +209,7 @@ struct Xchg {
                                    // round's count (pack), its unpack publishes total[applied]
     uint32_t hin;                  // push-sum tail round: the round kernel writes the halo faces
                                    // (k_ps_quiet_x<true>; k_shard_halo is not launched)
+    const char* rbase;             // the receive buffer (the unpack's message references count from it)
     uint32_t abnd[kMaxWorld + 1];  // actor range of every rank
     uint32_t sbnd[kMaxWorld + 1];  // link-slot range of every rank (global CSR numbering)
     uint32_t* pcount;              // entry counters of the current round, (peer, sub) then (world +

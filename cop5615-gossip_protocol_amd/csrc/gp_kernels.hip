@@ -260,6 +260,7 @@ constexpr uint32_t kLinkUnroll = GP_LINK_UNROLL;
 #define GP_GRID_LOADS 3
 #endif
 constexpr uint32_t kGridLoads = GP_GRID_LOADS;
+
 static_assert(kGridLoads >= 1 && kGridLoads <= 6, "GP_GRID_LOADS: 1 .. 6");
 // One GPU: message loads issued for the first GP_FIRED_LOADS fired link slots of an actor, the
 // others on demand (GP_LINK_UNROLL: one per unrolled slot, fired or not).  1: C3 -3%, 100M -1%
@@ -467,7 +468,8 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
             uint32_t ls[kLinkUnroll];
             bool lk[kLinkUnroll];
             double2 lm[kLinkUnroll];
-            uint8_t lc[kLinkUnroll];
+            uint32_t lc[kLinkUnroll];
+            uint32_t lr[kLinkUnroll];  // LM 2: the slots' references
             static_assert(kLinkUnroll == 4, "GP_LINK_UNROLL: the slots load as one 16-byte load");
             {
                 // the four unrolled slots' sources as one 16-byte load and their marks as two
@@ -480,26 +482,42 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                 ls[1] = s4.y;
                 ls[2] = s4.z;
                 ls[3] = s4.w;
-                const uint32_t* mw = reinterpret_cast<const uint32_t*>(a.lcnt_prev + (li & ~3u));
-                const uint64_t m8 = (uint64_t)mw[0] | ((uint64_t)mw[1] << 32);
-                const uint32_t sh = 8u * (li & 3u);
+                if constexpr (LM == 2) {  // four 32-bit references, one 16-byte load like the sources
+                    u4v r4;
+                    __builtin_memcpy(&r4, &a.lref_prev[li], sizeof r4);
+                    lr[0] = r4.x;
+                    lr[1] = r4.y;
+                    lr[2] = r4.z;
+                    lr[3] = r4.w;
 #pragma unroll
-                for (uint32_t k = 0; k < 4; ++k) lc[k] = (uint8_t)(m8 >> (sh + 8u * k));
+                    for (uint32_t k = 0; k < 4; ++k) lc[k] = lr[k] & kRefTagMask;
+                } else {
+                    const uint32_t* mw = reinterpret_cast<const uint32_t*>(a.lcnt_prev + (li & ~3u));
+                    const uint64_t m8 = (uint64_t)mw[0] | ((uint64_t)mw[1] << 32);
+                    const uint32_t sh = 8u * (li & 3u);
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; ++k) lc[k] = (uint8_t)(m8 >> (sh + 8u * k));
+                }
             }
             // ---- level 3: the messages of the sources whose slot is marked
 #pragma unroll
             for (uint32_t k = 0; k < kLinkUnroll; ++k)
-                lk[k] = k < nl && lc[k] == a.tag_prev;  // round tags
+                lk[k] = k < nl && lc[k] == (LM == 2 ? a.rtag_prev : a.tag_prev);  // round tags
             if constexpr (LM != 0 && kFiredLoads < kLinkUnroll && FF) {
                 // load the messages of the first kFiredLoads FIRED slots only (about one slot in
                 // seven fires: 0.14 messages per actor), the rest on demand (rare).  A shard reads
-                // a remote source's message from the receiver's slot (rmsg_prev), a local one from
-                // the source's row: one load through a selected address.
+                // a remote source's message from the receive buffer its slot's reference points into,
+                // a local one from the source's row: one load through a selected address.
                 uint32_t rest = 0;
 #pragma unroll
                 for (uint32_t k = 0; k < kLinkUnroll; ++k) rest |= lk[k] ? 1u << k : 0u;
                 auto msg_of = [&](uint32_t k, uint32_t u) -> const double2* {
-                    if (LM == 2 && (u < a.olo || u >= a.ohi)) return a.rmsg_prev + (li + k);
+                    if (LM == 2 && (u < a.olo || u >= a.ohi)) {
+                        uint32_t rf = lr[0];
+#pragma unroll
+                        for (uint32_t q = 1; q < kLinkUnroll; ++q) rf = k == q ? lr[q] : rf;
+                        return a.rin_prev + (rf >> kRefShift);
+                    }
                     return a.msg_prev + u;
                 };
                 uint32_t fs[kFiredLoads];
@@ -538,7 +556,7 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                                               // so the load goes out with the sources and marks
                         lm[k] = load_sel(a.rmsg_prev, k < nl, li + k, a.slot_lo);
                     } else if (LM == 2 && lk[k] && (ls[k] < a.olo || ls[k] >= a.ohi)) {
-                        lm[k] = a.rmsg_prev[li + k];
+                        lm[k] = a.rin_prev[lr[k] >> kRefShift];
                     } else {
                         lm[k] = load_sel(a.msg_prev, lk[k], ls[k], a.lo);
                     }
@@ -551,10 +569,12 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                     }
             }
             for (uint32_t k = kLinkUnroll; k < nl; ++k) {  // rare: more than kLinkUnroll sources
-                if (a.lcnt_prev[li + k] == a.tag_prev) {
+                const uint32_t rf = LM == 2 ? a.lref_prev[li + k] : 0u;
+                if (LM == 2 ? (rf & kRefTagMask) == a.rtag_prev : a.lcnt_prev[li + k] == a.tag_prev) {
                     const uint32_t u = a.rev_src[li + k];
                     flush(u);
-                    add(LM == 3 || (LM == 2 && (u < a.olo || u >= a.ohi)) ? a.rmsg_prev[li + k] : a.msg_prev[u]);
+                    add(LM == 3 ? a.rmsg_prev[li + k]
+                                : LM == 2 && (u < a.olo || u >= a.ohi) ? a.rin_prev[rf >> kRefShift] : a.msg_prev[u]);
                 }
             }
         }
@@ -792,7 +812,7 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
                     const Xchg& x = *xp;
                     const uint32_t lp = load_sel(a.lpos, ls.fired, u, a.lo);
                     const bool remote = ls.fired && (lp < x.sbnd[x.rank] || lp >= x.sbnd[x.rank + 1]);
-                    if (ls.fired && !remote) a.lcnt_cur[lp] = (uint8_t)a.tag_cur;
+                    if (ls.fired && !remote) a.lref_cur[lp] = a.rtag_cur;
                     const uint32_t q = remote ? owner(x.sbnd, x.world, lp) : 0u;
                     const uint32_t pos = wave_reserve(x, remote, q);
                     if (remote) put<true>(x, q, pos, lp, ls.msg);
@@ -1037,9 +1057,9 @@ __device__ __forceinline__ void block_reserve(const Xchg& x, const bool (&want)[
 // block-level reservations (three barriers and one global atomic per peer each).
 constexpr uint32_t kShardPer = 4;
 
-// Sharded push-sum link pass: a link message whose CSR slot is this rank's gets the slot's link
-// count (the receiver reads msg_prev[u] itself, as on one GPU); one whose slot belongs to another
-// rank goes to that rank's send chunk as (global slot, s, w), written into the same slot there.
+// Sharded push-sum link pass: a link message whose CSR slot is this rank's gets the slot's round tag
+// (the receiver reads msg_prev[u] itself, as on one GPU); one whose slot belongs to another rank goes
+// to that rank's send chunk as (global slot, s, w), and the receiver's unpack points the slot at it.
 __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg x) {
     if (applied_converged(a)) return;  // block-uniform: F(r) was a no-op
     const uint32_t n = a.hi < a.g.wired ? a.hi : a.g.wired;
@@ -1070,7 +1090,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg 
     uint32_t q[kShardPer], pos[kShardPer];
 #pragma unroll
     for (uint32_t j = 0; j < kShardPer; ++j) {
-        if (l[j] && !rm[j]) a.lcnt_cur[lp[j]] = (uint8_t)a.tag_cur;
+        if (l[j] && !rm[j]) a.lref_cur[lp[j]] = a.rtag_cur;
         q[j] = rm[j] ? owner(x.sbnd, x.world, lp[j]) : 0u;
     }
     block_reserve(x, rm, q, pos);
@@ -1389,10 +1409,11 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
                 if (!(a.dbits && ((a.dbits[t >> 5] >> (t & 31u)) & 1u))) atomicAdd(&a.inc_cur[t], 1u);
             }
             else if (gossip) a.lcnt_cur[t] = (uint8_t)((e >> 31) + 1u);
-            else {  // the sender's message into the receiver's slot, the slot marked
-                a.rmsg_cur[t] = in.msg[i];
-                a.lcnt_cur[t] = (uint8_t)a.tag_cur;  // plain: non-temporal marks and messages
-                                                     // cost 0.29 ms more per round (C5 / 8)
+            else {  // the slot points at the message where it arrived: one 4-byte store per entry (the
+                    // message and a mark were two scattered stores, 16 + 1 bytes: 0.6 + 0.2 ms of a 0.9 ms
+                    // unpack at C5 / 8, profiles/round5/unpack_write_ab/)
+                const uint32_t at = (uint32_t)((reinterpret_cast<const char*>(in.msg + i) - x.rbase) >> 4);
+                a.lref_cur[t] = a.rtag_cur | (at << kRefShift);
                 if (mark) a.act_cur[x.slot_dst[t] >> kActShift] = mtag;  // the receiver owning slot t
             }
         }
@@ -2450,7 +2471,7 @@ void launch_ps_pull(const RoundArgs& a, const Launch& l, const Xchg* x) {
         else hipLaunchKernelGGL((k_ps_pull<0, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
     } else if (a.rmsg_prev && !a.sharded) {  // one GPU, small graph: link messages by slot
         hipLaunchKernelGGL((k_ps_pull<3, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
-    } else if (a.rmsg_prev) {  // a shard of several ranks
+    } else if (a.lref_prev) {  // a push-sum shard (slot references)
         if (q && x->hin) hipLaunchKernelGGL(k_ps_quiet_x<true>, dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a, *x);
         else if (q) hipLaunchKernelGGL(k_ps_quiet_x<false>, dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a, *x);
         else hipLaunchKernelGGL((k_ps_pull<2, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);

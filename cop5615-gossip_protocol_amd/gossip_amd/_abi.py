@@ -13,7 +13,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, os.environ.get("GP_LIB", "lib"), "libgossip_hip.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "gossip_hip.h")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 TOPOLOGIES = {"line": 0, "full": 1, "2D": 2, "Imp3D": 3, "3D": 4}
 ALGOS = {"gossip": 0, "push-sum": 1}
 FLAG_KERNEL_TIMING = 1

@@ -92,8 +92,16 @@ class HipShard:
         # aligned blocks (the ABI needs 256)
         st, rt = int(self.shard.send_total), int(self.shard.recv_total)
         self.send_buf = torch.zeros(max(1, st), dtype=torch.uint8, device=dev)[:st]
-        self.recv_buf = torch.zeros(max(1, rt), dtype=torch.uint8, device=dev)[:rt]
+        # two receive buffers, one per round parity: a push-sum round reads the previous round's remote
+        # messages where they arrived, and in pieces the next exchange overlaps it
+        self._recv = [torch.zeros(max(1, rt), dtype=torch.uint8, device=dev)[:rt] for _ in range(2)]
+        self._ri = 0
         self.status = _abi.Status()
+
+    @property
+    def recv_buf(self):
+        """The receive buffer of the round in progress (the exchange writes it, deliver() reads it)."""
+        return self._recv[self._ri]
 
     def _plan(self):
         """The next round's per-peer chunk sizes (gp_shard_plan): they follow the activity of the
@@ -148,6 +156,7 @@ class HipShard:
 
     def deliver(self):
         _abi.check(self.lib.gp_shard_deliver(self.h, C.c_void_p(self.recv_buf.data_ptr())))
+        self._ri ^= 1
 
     def sync(self):
         _abi.check(self.lib.gp_shard_sync(self.h, C.byref(self.status)))

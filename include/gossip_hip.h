@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 6
+#define GP_ABI_VERSION 7
 
 /* program.fs:151 "line", :191 "full", :227 "2D", :267 "Imp3D"; "3D" is build-defined (Q9) */
 enum gp_topology { GP_LINE = 0, GP_FULL = 1, GP_TWO_D = 2, GP_IMP3D = 3, GP_THREE_D = 4 };
@@ -217,7 +217,12 @@ int gp_shard_pieces(void* handle);
 int gp_shard_round_piece(void* handle, void* send_buf, int32_t piece);
 int gp_shard_plan_piece(void* handle, int32_t piece, int64_t* send_bytes, int64_t* recv_bytes, int64_t* offsets);
 /* Enqueue the unpacking of what the other ranks sent for that round (recv_buf: recv_total
- * bytes of device memory).  Must follow each gp_shard_round.  Asynchronous. */
+ * bytes of device memory, 256-byte aligned).  Must follow each gp_shard_round.  Asynchronous.
+ * ABI 7: a push-sum shard's next round reads the remote link messages where they arrived (the slots
+ * keep references into recv_buf), so round k's receive buffer must stay unchanged
+ * until round k+1's kernels have run: with one piece an exchange that is stream-ordered after
+ * gp_shard_round may reuse it; in pieces (where round k+1's exchange overlaps its kernels) the host
+ * alternates two buffers — the same buffer twice in a row fails with GP_EINVAL. */
 int gp_shard_deliver(void* handle, const void* recv_buf);
 /* Wait for the enqueued rounds and fill st from the global completion counts (st->sum_s /
  * sum_w are this rank's share), then choose the next batch's plan (gp_shard_plan).  If a reduced

@@ -84,7 +84,7 @@ def test_kstats_struct_layout():
     assert names == [f[0] for f in _abi.KStats._fields_] == [
         "launches", "total_ms", "avg_ms", "bytes_per_launch", "kernel", "aux_avg_ms", "aux_kernel", "work_per_launch"]
     assert _abi.KStats.work_per_launch.offset == 168 and C.sizeof(_abi.KStats) == 176
-    assert _abi.ABI_VERSION == 6 and re.search(r"#define GP_ABI_VERSION 6\b", text)
+    assert _abi.ABI_VERSION == 7 and re.search(r"#define GP_ABI_VERSION 7\b", text)
 
 
 def test_shard_counters_struct_layout():
