@@ -1342,8 +1342,12 @@ int shard_deliver(Handle* h, const void* recv) {
         const Xchg x = make_xchg(h, h->pending_send, recv, i);
         // the grid covers the largest per-peer part: link entries, a halo face, or (full gossip) a
         // peer's done-bitmap words, which arrive whole whatever the plan
-        const bool face = i == 0 || i == h->npiece - 1;  // (the halo faces travel in the end pieces)
-        uint32_t most = std::max(kSub * h->max_in_cap[i], face ? h->halo : 0u);
+        // (the halo faces travel in the end pieces; the whole grid strides over a face, so it needs
+        // 1/world of it per peer: a tail round's grid was world x the face in workgroups, 3 us of a
+        // 16 us unpack at 100M / 8, profiles/round5/unpack_grid/)
+        const bool face = i == 0 || i == h->npiece - 1;
+        const uint32_t per_face = (h->halo + (uint32_t)h->world - 1u) / (uint32_t)h->world;
+        uint32_t most = std::max(kSub * h->max_in_cap[i], face ? per_face : 0u);
         if (h->gossip && h->full)
             for (int q = 0; q < h->world; ++q) most = std::max(most, (uint32_t)((h->abnd[q + 1] - h->abnd[q]) / 32 + 2));
         launch_shard_unpack(h->args((uint32_t)k), x, applied_round(h, k), most, h->gossip ? 1 : 0, h->full ? 1 : 0,
