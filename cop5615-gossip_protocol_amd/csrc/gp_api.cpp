@@ -1892,7 +1892,11 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
                 GsTally& t = h->tally;
                 t.nb = nb;
                 t.W = (uint32_t)h->grid;
-                t.thr = (cfg->flags & GP_FLAG_GOSSIP_TALLY) ? 0u : (uint32_t)std::min<size_t>(n / kTallyThrDiv, 0xFFFFFFFFu);
+                // (from kDsumMinActors a quarter of it: the ramp's last atomic round, 27M receipts at C4,
+                // tallies too; C4 46.06 -> 45.50 ms, 10M unchanged with 8 (+3% with 32),
+                // profiles/round5/cli/c4_tally_thr_*.txt)
+                const size_t div = kTallyThrDiv * (n >= kDsumMinActors ? 4u : 1u);
+                t.thr = (cfg->flags & GP_FLAG_GOSSIP_TALLY) ? 0u : (uint32_t)std::min<size_t>(n / div, 0xFFFFFFFFu);
                 const size_t nc = (size_t)nb * t.W;
                 if ((rc = h->alloc(&t.cnt, nc)) || (rc = h->alloc(&t.off, nc + 1)) || (rc = h->alloc(&t.tgt, 2 * n)) ||
                     (rc = h->alloc(&t.scratch, scan_scratch_words((uint32_t)nc))) ||
