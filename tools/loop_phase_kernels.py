@@ -4,7 +4,7 @@ kernel's launches (world per round, or world x pieces for a round in pieces, aft
 rounds), and each round to a phase by the global completion count before it (the run's trace from
 --series).
 
-    python3 tools/loop_phase_kernels.py KT_CSV SERIES_JSON ROUND_KERNEL [world]
+    python3 tools/loop_phase_kernels.py KT_CSV SERIES_JSON ROUND_KERNEL [world] [warmup rounds, default 8]
 """
 import bisect
 import csv
@@ -21,11 +21,12 @@ def name(r):
 def main():
     kt, series, rk = sys.argv[1:4]
     world = int(sys.argv[4]) if len(sys.argv) > 4 else 8
+    warm = int(sys.argv[5]) if len(sys.argv) > 5 else 8
     d = json.load(open(series))
     trace, nodes = d["trace"], None
     rows = sorted(csv.DictReader(open(kt)), key=lambda r: int(r["Start_Timestamp"]))
     # launches of the round kernel per round: world x the round's pieces (8 warm-up rounds first)
-    pieces = [d.get("warmup_pieces", 1)] * 8 + d.get("pieces_per_round", [])
+    pieces = [d.get("warmup_pieces", 1)] * warm + d.get("pieces_per_round", [1] * len(d["trace"]))
     starts, acc = [], 0
     for k in pieces:
         starts.append(acc)
@@ -36,9 +37,9 @@ def main():
         n = name(r)
         if n == rk or n.startswith(rk + "<"):  # (k_ps_quiet_x<false> / <true>)
             if seen < acc:
-                rnd = bisect.bisect_right(starts, seen) - 1 - 8
+                rnd = bisect.bisect_right(starts, seen) - 1 - warm
             else:  # launched past the recorded rounds (one piece each)
-                rnd = len(pieces) - 8 + (seen - acc) // world
+                rnd = len(pieces) - warm + (seen - acc) // world
             seen += 1
         if rnd < 0:
             continue
