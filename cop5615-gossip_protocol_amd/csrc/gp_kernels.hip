@@ -201,19 +201,22 @@ __device__ __forceinline__ void put(const Xchg& x, uint32_t q, uint32_t pos, uin
 // the sub-segment counter of peer q (the quiet-tail rounds of a shard, where entries are few and the
 // walk is per wave).  Every lane of the wave must call it.
 __device__ __forceinline__ uint32_t wave_reserve(const Xchg& x, bool want, uint32_t q) {
-    uint32_t pos = 0;
-    uint64_t left = __ballot(want);
-    while (left) {  // wave-uniform: one peer per trip
+    uint64_t left = __ballot(want), mine = 0;
+    if (!left) return 0;
+    while (left) {  // wave-uniform: the lanes of one peer per trip (ballots only, no memory)
         const uint32_t lead = (uint32_t)__builtin_ctzll(left);
         const uint32_t pq = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)lead);
         const uint64_t m = __ballot(want && q == pq);
-        uint32_t base = 0;
-        if ((threadIdx.x & 63u) == lead) base = atomicAdd(ctr_at(x, pq, my_sub()), (uint32_t)__popcll(m));
-        base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)lead);
-        if (want && q == pq) pos = base + mbcnt64(m);
+        if (want && q == pq) mine = m;
         left &= ~m;
     }
-    return pos;
+    // one atomic per peer, all in flight together (one after another, each waited for, they put a
+    // returning atomic's latency per peer into a tail pass)
+    const uint32_t lead = (uint32_t)__builtin_ctzll(mine | (1ull << 63));
+    uint32_t base = 0;
+    if (want && (threadIdx.x & 63u) == lead) base = atomicAdd(ctr_at(x, q, my_sub()), (uint32_t)__popcll(mine));
+    base = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead << 2), (int)base);
+    return want ? base + mbcnt64(mine) : 0u;
 }
 
 // ------------------------------------------------------------------ push-sum, grid topologies
@@ -806,28 +809,36 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
             }
             if constexpr (LM == 2) {
                 // A shard's tail round routes its own link messages (k_ps_link_scatter_x skips these
-                // rounds): a slot of this rank gets its mark, another rank's an entry of its chunk,
-                // positions reserved per wave (the tail's entries are few).  Wave-uniform here.
+                // rounds): a slot of this rank gets its mark, another rank's an entry of its chunk.
+                // HIN: it also writes the halo faces (k_shard_halo's work), the direction byte of every
+                // face actor and an entry for each message that crosses.  A message takes one way, so
+                // a lane needs at most one position: one reservation per wave and pass, positions
+                // reserved per wave (the tail's entries are few).  Wave-uniform here.
                 if (tail) {
                     const Xchg& x = *xp;
                     const uint32_t lp = load_sel(a.lpos, ls.fired, u, a.lo);
                     const bool remote = ls.fired && (lp < x.sbnd[x.rank] || lp >= x.sbnd[x.rank + 1]);
                     if (ls.fired && !remote) a.lref_cur[lp] = a.rtag_cur;
-                    const uint32_t q = remote ? owner(x.sbnd, x.world, lp) : 0u;
-                    const uint32_t pos = wave_reserve(x, remote, q);
-                    if (remote) put<true>(x, q, pos, lp, ls.msg);
-                }
-            }
-            if constexpr (LM == 2 && HIN) {  // the halo faces (k_shard_halo's work; wave-uniform here)
-                const Xchg& x = *xp;
-                const bool own = u - a.lo < a.hi - a.lo;
+                    uint32_t q = remote ? owner(x.sbnd, x.world, lp) : 0u;
+                    bool cross = false;
+                    uint32_t fo = 0, sd = 0;
+                    if constexpr (HIN) {
+                        const bool own = u - a.lo < a.hi - a.lo;
 #pragma unroll
-                for (uint32_t sd = 0; sd < 2; ++sd) {
-                    const uint32_t fo = u - x.h.out_first[sd];
-                    const bool face = own && fo < x.h.out_n[sd];
-                    if (face) x.h.out_dir[sd][fo] = (uint8_t)ls.dir;
-                    const bool cross = face && ls.dir == x.h.code[sd];
-                    const uint32_t pos = wave_reserve(x, cross, x.world + sd);
+                        for (uint32_t k = 0; k < 2; ++k) {
+                            const uint32_t o = u - x.h.out_first[k];
+                            const bool face = own && o < x.h.out_n[k];
+                            if (face) x.h.out_dir[k][o] = (uint8_t)ls.dir;
+                            if (face && ls.dir == x.h.code[k]) {
+                                cross = true;
+                                fo = o;
+                                sd = k;
+                            }
+                        }
+                        if (cross) q = x.world + sd;
+                    }
+                    const uint32_t pos = wave_reserve(x, remote || cross, q);
+                    if (remote) put<true>(x, q, pos, lp, ls.msg);
                     if (cross) {
                         const uint32_t cap = x.h.out_cap[sd];
                         if (pos < cap) {

@@ -4,7 +4,10 @@ kernel's launches (world per round, or world x pieces for a round in pieces, aft
 rounds), and each round to a phase by the global completion count before it (the run's trace from
 --series).
 
-    python3 tools/loop_phase_kernels.py KT_CSV SERIES_JSON ROUND_KERNEL [world] [warmup rounds, default 8]
+    python3 tools/loop_phase_kernels.py KT_CSV SERIES_JSON ROUND_KERNEL [world] [warmup rounds, default 8] [bucket]
+
+bucket: also the tail's rounds in buckets of that many (converged share, kernels and round kernel
+per rank-round).
 """
 import bisect
 import csv
@@ -22,6 +25,7 @@ def main():
     kt, series, rk = sys.argv[1:4]
     world = int(sys.argv[4]) if len(sys.argv) > 4 else 8
     warm = int(sys.argv[5]) if len(sys.argv) > 5 else 8
+    bucket = int(sys.argv[6]) if len(sys.argv) > 6 else 0
     d = json.load(open(series))
     trace, nodes = d["trace"], None
     rows = sorted(csv.DictReader(open(kt)), key=lambda r: int(r["Start_Timestamp"]))
@@ -59,6 +63,14 @@ def main():
         print(f"{label}: {len(rs)} rounds, kernels per rank-round {tot:.1f} us, per rank over these rounds {tot * len(rs) / 1e3:.2f} ms")
         for k in ks:
             print(f"  {k:48s} {statistics.fmean(per[r].get(k, 0.0) for r in rs) / world:9.2f} us")
+    if bucket:
+        tail = sorted(r for r in per if r < len(prev) and prev[r] * 100 >= 99 * nodes)
+        print(f"tail by {bucket} rounds: rounds, not converged before, kernels / round kernel per rank-round (us)")
+        for i in range(0, len(tail), bucket):
+            rs = tail[i:i + bucket]
+            rkt = statistics.fmean(sum(v for k, v in per[r].items() if k == rk or k.startswith(rk + "<")) for r in rs)
+            tot = statistics.fmean(sum(per[r].values()) for r in rs)
+            print(f"  {rs[0]:5d}..{rs[-1]:<5d} {1 - prev[rs[0]] / nodes:8.5f} {tot / world:8.1f} {rkt / world:8.1f}")
 
 
 if __name__ == "__main__":
