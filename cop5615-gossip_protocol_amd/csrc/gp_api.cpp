@@ -29,6 +29,10 @@ constexpr size_t kTallyMinActors = 1u << 20;
 // Small Imp3D push-sum graphs on one GPU (no quiet marks): link senders also write their message into
 // the receiver's CSR slot (k_ps_pull<3>)
 constexpr uint32_t kSlotMsgMaxActors = 1u << 18;
+// Small one-GPU line grids (line / 2D push-sum) below this many actors (the quiet tail's threshold)
+// run up to kTileMaxNR rounds per launch
+// (k_ps_tile); GP_FLAG_ONE_ROUND keeps one round per launch.
+constexpr uint32_t kTileMaxActors = 1u << 20;
 #ifndef GP_TALLY_THR_DIV
 #define GP_TALLY_THR_DIV 8
 #endif
@@ -222,9 +226,18 @@ struct Handle {
     const void* msg_src = nullptr;           // the receive buffer the next round reads remote messages from
     uint32_t* slot_dst = nullptr;            // shards with the quiet tail: receiver of each own CSR slot
     // push-sum
-    double2* msg[2] = {nullptr, nullptr};
-    uint8_t* dir[2] = {nullptr, nullptr};
+    double2* msg[kTileBufs] = {};
+    uint8_t* dir[kTileBufs] = {};
     uint8_t* flags = nullptr;
+    // small one-GPU line grids: several rounds per launch (k_ps_tile);
+    // msg / dir / flags then rotate over kTileBufs buffers, round k's state in [k mod kTileBufs]
+    bool tiles = false;
+    uint8_t* flg[kTileBufs] = {};
+    TileArgs tl{};
+    int nbuf() const { return tiles ? (int)kTileBufs : 2; }
+    // the buffer of round k's state (k = -1: the initial state)
+    int bidx(int64_t k) const { return (int)((k + nbuf()) % nbuf()); }
+    uint8_t* flags_at(int64_t k) const { return tiles ? flg[bidx(k)] : flags; }
     double2* frozen = nullptr;
     uint8_t* act[2] = {nullptr, nullptr};  // quiet-wave marks, one byte per 64 actors (ping-pong)
     uint32_t act_thr = 0;
@@ -337,10 +350,11 @@ struct Handle {
         a.rev_src = rev_src;
         a.lpos = lpos;
         const int c = (int)(r & 1u), p = c ^ 1;
+        const int cm = bidx(r), pm = bidx((int64_t)r - 1);  // msg / dir (kTileBufs buffers with tiles)
         a.lcnt_prev = lcnt[p];
         a.lcnt_cur = lcnt[c];
-        a.msg_prev = msg[p];
-        a.msg_cur = msg[c];
+        a.msg_prev = msg[pm];
+        a.msg_cur = msg[cm];
         a.rmsg_prev = rmsg[p];
         a.rmsg_cur = rmsg[c];
         a.lref_prev = lref[p];
@@ -348,10 +362,10 @@ struct Handle {
         a.rtag_prev = r ? ref_tag(r - 1u) : 0u;
         a.rtag_cur = ref_tag(r);
         a.rin_prev = static_cast<const double2*>(msg_src);
-        a.dir_prev = dir[p];
-        a.dir_cur = dir[c];
+        a.dir_prev = dir[pm];
+        a.dir_cur = dir[cm];
         a.work = (cfg.flags & GP_FLAG_KERNEL_TIMING) && act[0] ? work : nullptr;
-        a.flags = flags;
+        a.flags = flags_at((int64_t)r - 1);
         a.frozen = frozen;
         if (gossip) {
             a.cnt = cnt;
@@ -573,14 +587,15 @@ int reset(Handle* h) {
     }
     h->msg_src = nullptr;
     if (!h->gossip) {
-        launch_ps_init(h->flags, h->g, h->lo, h->hi, h->full ? 1u : 0u, (uint32_t)h->cfg.term_init, h->L());
+        for (int i = 0; i < (h->tiles ? h->nbuf() : 1); ++i)  // (tiles: every buffer; non-participants keep theirs)
+            launch_ps_init(h->tiles ? h->flg[i] : h->flags, h->g, h->lo, h->hi, h->full ? 1u : 0u,
+                           (uint32_t)h->cfg.term_init, h->L());
         if (h->generic) {
             HIP_TRY(hipMemsetAsync(h->bcnt[0] + lo, 0, n * sizeof(uint32_t), h->stream));
             HIP_TRY(hipMemsetAsync(h->bcnt[1] + lo, 0, n * sizeof(uint32_t), h->stream));
             HIP_TRY(hipMemsetAsync(h->tgt + lo, 0xFF, n * sizeof(uint32_t), h->stream));
         } else {
-            launch_fill_u8(h->dir[0] + xlo, kDirNone, xn, h->stream);
-            launch_fill_u8(h->dir[1] + xlo, kDirNone, xn, h->stream);
+            for (int i = 0; i < h->nbuf(); ++i) launch_fill_u8(h->dir[i] + xlo, kDirNone, xn, h->stream);
             for (int i = 0; i < 2; ++i) {
                 int rc;
                 if (h->act[i] && (rc = clear_act(h, i))) return rc;
@@ -682,6 +697,7 @@ const char* round_kernel_name(const Handle* h) {
     if (h->sharded && h->g.has_link && h->lref[0]) return h->act[0] ? "k_ps_quiet_x" : "k_ps_pull<2, false>";
     if (h->g.has_link && h->rmsg[0]) return "k_ps_pull<3, false>";
     if (h->g.has_link) return h->act[0] ? "k_ps_quiet<1>" : "k_ps_pull<1, false>";
+    if (h->tiles) return "k_ps_tile";
     return h->act[0] ? "k_ps_quiet<0>" : "k_ps_pull<0, false>";
 }
 
@@ -740,8 +756,12 @@ void piece_args(const Handle* h, int piece, RoundArgs& a, Launch& l) {
     a.span = span_for(a.hi - a.lo, l.grid);
 }
 
-void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed, int piece = 0) {
+void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed, int piece = 0, int nr = 1) {
     RoundArgs a = h->args((uint32_t)k);
+    if (h->tiles) {
+        launch_ps_tile(a, h->tl, nr, h->stream);
+        return;
+    }
     if (h->sharded && !timed) a.work = nullptr;
     Launch l = h->L();
     piece_args(h, piece, a, l);
@@ -833,13 +853,13 @@ int clear_act_if_due(Handle* h, int64_t k) {
 // Round k with its three timing events (slot i of the event ring).
 // (In pieces, the events bracket the whole round: piece 0's round kernel to the last piece's round
 // kernel, then the last piece's pass; the earlier pieces' passes count as round kernel time.)
-int launch_round(Handle* h, int64_t k, const Xchg* x, bool timing, int64_t i, int piece = 0) {
+int launch_round(Handle* h, int64_t k, const Xchg* x, bool timing, int64_t i, int piece = 0, int nr = 1) {
     int rc;
     const bool first = piece == 0, last = piece == h->npiece - 1;
     if (first && (fused_marks(h) || h->sharded) && (rc = clear_tags_if_due(h, (uint32_t)k))) return rc;
     if (first && (rc = clear_act_if_due(h, k))) return rc;
     if (timing && first) HIP_TRY(hipEventRecord(h->kev[3 * i], h->stream));
-    launch_main(h, k, x, timing, piece);
+    launch_main(h, k, x, timing, piece, nr);
     if (timing && last) HIP_TRY(hipEventRecord(h->kev[3 * i + 1], h->stream));
     if ((rc = launch_aux(h, k, x, piece))) return rc;
     if (timing && last) HIP_TRY(hipEventRecord(h->kev[3 * i + 2], h->stream));
@@ -862,8 +882,9 @@ int fill_sums(Handle* h, gp_status* st) {
     if (h->gossip) return GP_OK;
     const int64_t last = h->rounds - 1;
     RoundArgs a = h->args((uint32_t)std::max<int64_t>(last, 0));
-    a.msg_prev = h->msg[last >= 0 ? (last & 1) : 0];
-    a.dir_prev = h->generic ? nullptr : h->dir[last >= 0 ? (last & 1) : 0];
+    a.msg_prev = h->msg[h->bidx(std::max<int64_t>(last, 0))];
+    a.dir_prev = h->generic ? nullptr : h->dir[h->bidx(std::max<int64_t>(last, 0))];
+    a.flags = h->flags_at(last);
     launch_ps_sums(a, last >= 0 ? 1u : 0u, h->partials, h->L());
     std::vector<double2> part((size_t)h->grid);
     HIP_TRY(hipMemcpyAsync(part.data(), h->partials, part.size() * sizeof(double2), hipMemcpyDeviceToHost, h->stream));
@@ -899,11 +920,16 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         const int64_t every = group ? kTimeGroup : kTimeEvery;
         const int64_t ng = (B + every - 1) / every;
         if (timing && (rc = ensure_events(h, ng))) return rc;
-        for (int64_t i = 0; i < B; ++i) {
+        for (int64_t i = 0; i < B;) {
             const int64_t j = i / every;
+            // tiles: up to kTileMaxNR rounds in one launch, within this batch and timing group
+            int nr = 1;
+            while (h->tiles && nr < (int)kTileMaxNR && i + nr < B && (i + nr) / every == j) ++nr;
             if (group && i % every == 0) HIP_TRY(hipEventRecord(h->kev[3 * j], h->stream));
-            if ((rc = launch_round(h, h->next_kernel + i, nullptr, timing && !group && i % every == 0, j))) return rc;
-            if (group && (i % every == every - 1 || i == B - 1)) {
+            if ((rc = launch_round(h, h->next_kernel + i, nullptr, timing && !group && i % every == 0, j, 0, nr)))
+                return rc;
+            i += nr;
+            if (group && (i % every == 0 || i == B)) {
                 HIP_TRY(hipEventRecord(h->kev[3 * j + 1], h->stream));
                 HIP_TRY(hipEventRecord(h->kev[3 * j + 2], h->stream));
             }
@@ -922,7 +948,8 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
             HIP_TRY(hipHostGetDevicePointer((void**)&h->d_trace, h->h_trace, 0));
             h->h_trace_cap = B;
         }
-        launch_finalize(h->total, h->parts, h->next_kernel - (h->gossip ? 2 : 1), h->stream, h->d_trace, h->rounds);
+        launch_finalize(h->total, h->parts, h->next_kernel - (h->gossip ? 2 : 1), h->stream, h->d_trace, h->rounds,
+                        h->tiles);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipStreamSynchronize(h->stream));
         int64_t real = B;
@@ -1939,6 +1966,19 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
         } else if ((rc = h->alloc(&h->dir[0], xn, xlo)) || (rc = h->alloc(&h->dir[1], xn, xlo))) {
             return bail(rc);
         }
+        h->tiles = !h->sharded && !h->generic && !g.has_link && g.gy == 1 && g.gz == 1 && !h->act[0] &&
+                   A < kTileMaxActors && !(cfg->flags & GP_FLAG_ONE_ROUND);
+        if (h->tiles) {
+            TileArgs& t = h->tl;
+            for (int i = 2; i < (int)kTileBufs; ++i)
+                if ((rc = h->alloc(&h->msg[i], xn, xlo)) || (rc = h->alloc(&h->dir[i], xn, xlo))) return bail(rc);
+            for (int i = 0; i < (int)kTileBufs; ++i) {
+                if ((rc = h->alloc(&h->flg[i], n, lo))) return bail(rc);
+                t.msg[i] = h->msg[i];
+                t.dir[i] = h->dir[i];
+                t.flg[i] = h->flg[i];
+            }
+        }
     }
     if (g.has_link && (rc = build_links(h))) return bail(rc);
     if (h->sharded && (rc = build_plan(h))) return bail(rc);
@@ -2497,10 +2537,10 @@ int gp_read_pushsum(void* handle, int64_t first, int64_t count, double* S, doubl
     HIP_TRY(hipStreamSynchronize(h->stream));
     std::vector<uint8_t> f;
     std::vector<double2> fr, ms;
-    if ((rc = copy_slice(h, f, (const uint8_t*)h->flags, first, count))) return rc;
-    if ((rc = copy_slice(h, fr, (const double2*)h->frozen, first, count))) return rc;
     const int64_t last = h->rounds - 1;
-    if (last >= 0 && (rc = copy_slice(h, ms, (const double2*)h->msg[last & 1], first, count))) return rc;
+    if ((rc = copy_slice(h, f, (const uint8_t*)h->flags_at(last), first, count))) return rc;
+    if ((rc = copy_slice(h, fr, (const double2*)h->frozen, first, count))) return rc;
+    if (last >= 0 && (rc = copy_slice(h, ms, (const double2*)h->msg[h->bidx(last)], first, count))) return rc;
     for (int64_t i = 0; i < count; ++i) {
         const uint32_t v = (uint32_t)(first + i);
         const bool part = h->full || presence(h->g, v) != 0u;
@@ -2541,12 +2581,12 @@ int gp_read_messages(void* handle, int64_t first, int64_t count, uint32_t* dst, 
     std::vector<uint32_t> t((size_t)count, kNone);
     std::vector<double2> ms;
     if (last >= 0) {
-        if ((rc = copy_slice(h, ms, (const double2*)h->msg[last & 1], first, count))) return rc;
+        if ((rc = copy_slice(h, ms, (const double2*)h->msg[h->bidx(last)], first, count))) return rc;
         if (h->generic) {
             if ((rc = copy_slice(h, t, (const uint32_t*)h->tgt, first, count))) return rc;
         } else {
             std::vector<uint8_t> d;
-            if ((rc = copy_slice(h, d, (const uint8_t*)h->dir[last & 1], first, count))) return rc;
+            if ((rc = copy_slice(h, d, (const uint8_t*)h->dir[h->bidx(last)], first, count))) return rc;
             for (int64_t i = 0; i < count; ++i) {
                 const uint32_t v = (uint32_t)(first + i);
                 t[i] = d[i] == kDirNone ? kNone

@@ -17,7 +17,7 @@ constexpr int kMaxGrid = 256 * GP_GRID_PER_CU;
 #endif
 constexpr int kParts = 64;          // completion sub-counters per round (one 64 B line each)
 constexpr int kPartStride = 16;     // u32 words between sub-counters
-constexpr int kPartRing = 4;        // rounds kept in the sub-counter ring
+constexpr int kPartRing = 32;       // rounds kept in the sub-counter ring (k_ps_tile uses 24 at once)
 constexpr int kWorkStride = 8;      // u64 words between the walked-actor sub-counters
 constexpr int kMaxWorld = 16;
 constexpr int kMaxPieces = 4;       // a shard's round in at most this many pieces
@@ -248,6 +248,19 @@ static_assert(kActSeg >= 2u && kActSeg < 64u, "segments of 2 .. 32 actors");
 
 // round kernels
 void launch_ps_pull(const RoundArgs& a, const Launch& l, const Xchg* x = nullptr);  // x: a shard of several ranks
+// Small one-GPU line grids (line / 2D push-sum): one launch runs rounds r .. r + nr - 1
+// (nr <= kTileMaxNR) of a segment of kTileSeg actors: round r + q over the segment and nr - 1 - q
+// actors either side of it, round r from round r - 1's state of the segment and nr actors either side
+// (loaded into LDS), each later round from the one before in LDS.  Round k's state is in buffer
+// [k mod kTileBufs] (round -1's: the last): a launch reads one buffer and writes nr others.
+constexpr uint32_t kTileMaxNR = 8, kTileBufs = kTileMaxNR + 1;
+struct TileArgs {
+    double2* msg[kTileBufs];
+    uint8_t* dir[kTileBufs];
+    uint8_t* flg[kTileBufs];
+};
+constexpr uint32_t kTileSeg = 256 - 2 * kTileMaxNR, kTileLoad = kTileSeg + 2 * kTileMaxNR;
+void launch_ps_tile(const RoundArgs& a, const TileArgs& t, int nr, hipStream_t s);
 void launch_gs_pull(const RoundArgs& a, const Launch& l);
 // Gossip grid rounds on graphs below 2^18 actors (one GPU) issue their level-1 loads ahead of
 // the gate: k_gs_pull<LINK, true>.  (At 1M actors the unconditional loads cost more than the
@@ -332,8 +345,9 @@ void launch_fill_u8(uint8_t* p, uint8_t v, size_t n, hipStream_t s);
 int launch_load(hipStream_t s);  // load the code object now (an empty kernel, synchronised): 0 ok
 // total[a] = total[a-1] + sum of the round-a sub-counters (after the last kernel of a batch)
 // (out: also total[first .. a] into out[], e.g. host-mapped memory)
+// pairs (k_ps_tile): total[a - 1] may be unwritten (round a - 1 was a launch's first round)
 void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hipStream_t s,
-                     unsigned long long* out = nullptr, long long first = 0);
+                     unsigned long long* out = nullptr, long long first = 0, bool pairs = false);
 void launch_ps_init(uint8_t* flags, const Geom& g, uint32_t lo, uint32_t hi, uint32_t full, uint32_t term_init,
                     const Launch& l);
 // push-sum sums for gp_status: per-block partials of held + in-flight (s, w)

@@ -882,6 +882,127 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PSQ_W
     ps_pull_body<2, true, HIN>(a, &x);
 }
 
+
+// ------------------------------------------------------------------ small line grids: rounds in batches
+// (TileArgs)  A small grid's round is one latency-bound launch (gate, one load level,
+// stores); on a line (line and 2D topologies) one launch runs up to kTileMaxNR rounds of a segment:
+// round r + q over the segment and NR - 1 - q actors either side of it, round r from round r - 1's
+// state of the segment and NR actors either side (loaded into LDS), each later round from the one
+// before in LDS.  The rim is computed by both segments that border it, identically (the same
+// arithmetic on the same inputs).  Each segment writes every round's state of its own actors (round
+// r + q is the run's state if it converges there: the host then ignores the later rounds, whose
+// buffers no reader uses).  100K line: 4.85 us per one-round launch, 9.2 us per four rounds; boxes
+// of a 3D grid recompute 2.3-3.4x their actors in the rim and were slower (profiles/round5/tiles/).
+// One actor's round from its neighbours' direction bytes and messages in LDS (cell c), in ascending
+// source order (slot order), as ps_finish sums them.
+__device__ __forceinline__ PsOut tile_actor(const RoundArgs& a, uint32_t r, uint32_t v, uint32_t m, uint32_t c,
+                                            const uint8_t* dir, const double2* msg, uint8_t& f, double2 held,
+                                            uint32_t& code) {
+    code = kth_bit(m, scale_draw(philox_x(v, r, kStreamPush, a.seed), popc(m)));
+    double ss = 0.0, ww = 0.0;
+    uint32_t cin = 0;
+    if (r) {
+        // a line's slots: v - 1 (slot 2, code 1), v + 1 (slot 3, code 0)
+        if ((m & 1u) && dir[c - 1u] == 1u) {
+            const double2 mm = msg[c - 1u];
+            ss += mm.x;
+            ww += mm.y;
+            ++cin;
+        }
+        if ((m & 2u) && dir[c + 1u] == 0u) {
+            const double2 mm = msg[c + 1u];
+            ss += mm.x;
+            ww += mm.y;
+            ++cin;
+        }
+    } else {
+        held = make_double2((double)v, 1.0);
+    }
+    return ps_update(f, held, ss, ww, cin, a.delta, a.term_limit);
+}
+
+template <int NR>
+__global__ __launch_bounds__(kBlock) void k_ps_tile(RoundArgs a, TileArgs t) {
+    static_assert(NR >= 1 && NR <= (int)kTileMaxNR && kTileLoad <= kBlock, "one load per thread");
+    __shared__ double2 s_msg[2][kTileLoad];
+    __shared__ uint8_t s_dir[2][kTileLoad], s_flg[2][kTileLoad];
+    __shared__ unsigned long long prev_s;
+    __shared__ uint32_t red[NR][kBlock / 64];  // each round's newly converged actors per wave
+    const uint32_t r = a.r, n = a.g.actors;
+    // this segment [s0, s1); cells: actors s0 - NR .. s1 + NR - 1 (those on the line)
+    const uint32_t s0 = blockIdx.x * kTileSeg, s1 = min(s0 + kTileSeg, n);
+    const uint32_t c0 = s0 >= (uint32_t)NR ? s0 - NR : 0u, c1 = min(s1 + NR, n);
+    const uint32_t i = threadIdx.x, v = c0 + i;
+    // the loads go out before the gate resolves (latency-bound rounds, as k_ps_pull's PRE)
+    {
+        const uint32_t pin = (r + kTileBufs - 1u) % kTileBufs;  // round r - 1's state
+        const bool in = v < c1;
+        const uint32_t vv = in ? v : c0;  // (unconditional loads; round 0 reads no neighbour)
+        const uint8_t d = t.dir[pin][vv], f = t.flg[pin][vv];
+        const double2 mm = t.msg[pin][vv];
+        if (i < kTileLoad) {
+            s_dir[0][i] = in ? d : (uint8_t)kDirNone;
+            s_flg[0][i] = f;
+            s_msg[0][i] = mm;
+        }
+    }
+    // completion counts after rounds r - kTileMaxNR .. r - 1 (the last launch's rounds, up to
+    // kTileMaxNR of them, have no total yet): block 0 writes them
+    if (threadIdx.x < 64) {
+        const uint32_t lane = threadIdx.x;
+        unsigned long long x = r > kTileMaxNR ? a.total[r - kTileMaxNR - 1u] : 0ull;
+#pragma unroll
+        for (uint32_t q = kTileMaxNR; q >= 1u; --q) {
+            if (r >= q) {
+                x += wave_sum(*part_slot(a.parts, (long long)r - q, lane));
+                if (blockIdx.x == 0 && lane == 0) a.total[r - q] = x;
+            }
+        }
+        if (lane == 0) prev_s = x;
+        if (blockIdx.x == 0)  // the next launch's sub-counters (ring: kPartRing >= 3 kTileMaxNR)
+            for (uint32_t q = 0; q < kTileMaxNR; ++q) *part_slot(a.parts, (long long)r + NR + q, lane) = 0u;
+    }
+    __syncthreads();
+    if (prev_s >= a.target) return;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+        // round r + q over the segment and NR - 1 - q actors either side, from LDS side q & 1
+        const uint32_t rq = r + (uint32_t)q, w = (uint32_t)(NR - 1 - q), in = (uint32_t)q & 1u, out = in ^ 1u;
+        const uint32_t lo = s0 >= w ? s0 - w : 0u, hi = min(s1 + w, n);
+        uint32_t newly = 0;
+        if (v >= lo && v < hi) {
+            const uint32_t m = presence(a.g, v);
+            uint8_t f = s_flg[in][i];
+            uint32_t code = kDirNone;
+            PsOut o{};
+            if (m) o = tile_actor(a, rq, v, m, i, s_dir[in], s_msg[in], f, s_msg[in][i], code);
+            const uint8_t d = m && o.send ? (uint8_t)code : (uint8_t)kDirNone;
+            if (m && v >= s0 && v < s1) {
+                const uint32_t pq = rq % kTileBufs;
+                if (o.send) t.msg[pq][v] = o.msg;
+                t.dir[pq][v] = d;
+                t.flg[pq][v] = f;
+                if (o.conv_now) a.frozen[v] = o.msg;
+                newly = o.conv_now ? 1u : 0u;
+            }
+            if (q + 1 < NR) {
+                s_dir[out][i] = d;
+                s_flg[out][i] = f;
+                s_msg[out][i] = o.msg;
+            }
+        }
+        newly = wave_sum(newly);
+        if ((threadIdx.x & 63u) == 0) red[q][threadIdx.x >> 6] = newly;
+        __syncthreads();  // round r + q in LDS
+    }
+    if (threadIdx.x < (uint32_t)NR) {  // one add per round and block (the counts of F, block_add's)
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kBlock / 64; ++w) c += red[threadIdx.x][w];
+        if (c) atomicAdd(part_slot(a.parts, (long long)r + threadIdx.x, blockIdx.x & (kParts - 1)), c);
+    }
+}
+
 // ------------------------------------------------------------------ gossip, grid topologies
 // dir byte = chain-0 code | chain-1 code << 4 (15 = no chain)
 __device__ __forceinline__ uint32_t nib_match(uint8_t b, uint32_t code) {
@@ -2474,6 +2595,21 @@ uint32_t span_for(uint32_t n, int grid) {
 #endif
 static int quiet_grid(const Launch& l) { return l.grid < 256 * GP_PSQ_PER_CU ? l.grid : 256 * GP_PSQ_PER_CU; }
 
+void launch_ps_tile(const RoundArgs& a, const TileArgs& t, int nr, hipStream_t s) {
+    const int boxes = (int)((a.g.actors + kTileSeg - 1) / kTileSeg);
+    static_assert(kTileMaxNR == 8, "one instantiation per round count");
+    switch (nr) {
+        case 8: hipLaunchKernelGGL(k_ps_tile<8>, dim3(boxes), dim3(kBlock), 0, s, a, t); break;
+        case 7: hipLaunchKernelGGL(k_ps_tile<7>, dim3(boxes), dim3(kBlock), 0, s, a, t); break;
+        case 6: hipLaunchKernelGGL(k_ps_tile<6>, dim3(boxes), dim3(kBlock), 0, s, a, t); break;
+        case 5: hipLaunchKernelGGL(k_ps_tile<5>, dim3(boxes), dim3(kBlock), 0, s, a, t); break;
+        case 4: hipLaunchKernelGGL(k_ps_tile<4>, dim3(boxes), dim3(kBlock), 0, s, a, t); break;
+        case 3: hipLaunchKernelGGL(k_ps_tile<3>, dim3(boxes), dim3(kBlock), 0, s, a, t); break;
+        case 2: hipLaunchKernelGGL(k_ps_tile<2>, dim3(boxes), dim3(kBlock), 0, s, a, t); break;
+        default: hipLaunchKernelGGL(k_ps_tile<1>, dim3(boxes), dim3(kBlock), 0, s, a, t);
+    }
+}
+
 void launch_ps_pull(const RoundArgs& a, const Launch& l, const Xchg* x) {
     constexpr unsigned lds = 0;
     const bool q = a.act_cur != nullptr;
@@ -2666,7 +2802,10 @@ void launch_fill_u8(uint8_t* p, uint8_t v, size_t n, hipStream_t s) {
 
 
 void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hipStream_t s, unsigned long long* out,
-                     long long first) {
+                     long long first, bool pairs) {
+    if (pairs)  // the last launch's earlier rounds have no total yet
+        for (long long b = std::max(a - (long long)kTileMaxNR + 1, 0ll); b < a; ++b)
+            hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, total, parts, b, nullptr, 0ll);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, total, parts, a, out, first);
 }
 

@@ -28,6 +28,7 @@ FLAG_TIGHT_TIERS = 256
 FLAG_TALLY_FALLBACKS = 512
 FLAG_PIECES = 1024
 FLAG_FORCE_PIECES = 2048
+FLAG_ONE_ROUND = 4096
 ERRORS = {-1: "GP_EINVAL", -2: "GP_ENOMEM", -3: "GP_EHIP", -4: "GP_ESTATE", -5: "GP_EOVERFLOW", -6: "GP_ERCCL"}
 
 

@@ -321,3 +321,55 @@ def test_full_gossip_tally_fallbacks_vs_oracle(n, seed, forced):
     assert gpu.kernel_stats()["kernel"] == "k_gs_full4+tally"  # the tally was built for this graph
     gpu.close()
     cpu.close()
+
+
+# Small one-GPU line grids (line, 2D) run two rounds per launch (k_ps_tile): batches
+# of every parity, so that pairs and single rounds alternate and a step can end after either round
+# of a pair; segment edges, the line's ends and tiny graphs.
+TILE_CASES = [
+    (1, "line", 1, None), (2, "line", 1, None), (3, "line", 2, None), (9, "2D", 3, None), (253, "line", 4, None),
+    (254, "2D", 5, None), (1000, "line", 6, None), (5000, "2D", 7, None), (20000, "line", 9, 1500),
+    (50000, "2D", 10, 1200), (260000, "line", 12, 600),
+]
+
+
+@pytest.mark.parametrize("n,topo,seed,cap", TILE_CASES)
+def test_tiles_vs_oracle(n, topo, seed, cap):
+    gpu, cpu = _pair(n, topo, "push-sum", seed, kernel_timing=True)
+    assert gpu.kernel_stats()["kernel"] == "k_ps_tile"
+    done = 0
+    for chunk in (1, 2, 3, 5, 8, 13, 64, 255):
+        gs, cs = gpu.step(chunk), cpu.step(chunk, threads=8)
+        done += chunk
+        assert (gs.round, gs.completed, gs.converged) == (cs.round, cs.completed, cs.converged)
+        check_same(gpu, cpu, "push-sum")
+        if gs.converged:
+            break
+    if not gs.converged:
+        rest = (cap or 1 << 30) - done
+        gs, cs = gpu.step(rest), cpu.step(rest, threads=8)
+        assert (gs.round, gs.completed, gs.converged) == (cs.round, cs.completed, cs.converged)
+        check_same(gpu, cpu, "push-sum")
+    if cap is None:
+        assert gs.converged
+    assert gs.sum_s == pytest.approx(cs.sum_s, rel=1e-12) and gs.sum_w == pytest.approx(cs.sum_w, rel=1e-12)
+    gpu.reset()  # a second run: the three state buffers start clean
+    gs2 = gpu.step(cs.round)
+    assert (gs2.round, gs2.completed) == (cs.round, cs.completed)
+    check_same(gpu, cpu, "push-sum")
+    gpu.close()
+    cpu.close()
+
+
+@pytest.mark.parametrize("topo", ["line", "2D"])
+def test_tiles_vs_one_round_c2(topo):
+    """C2 line / 2D to convergence (1481 rounds): two rounds per launch against one round per
+    launch (GP_FLAG_ONE_ROUND, pinned by the oracle above and by the fingerprints)."""
+    a = Simulator(100000, topo, "push-sum", seed=1)
+    b = Simulator(100000, topo, "push-sum", seed=1, one_round=True, kernel_timing=True)
+    assert b.kernel_stats()["kernel"] == "k_ps_pull<0, false>"
+    sa, sb = a.step(), b.step()
+    assert sa.converged and (sa.round, sa.completed) == (sb.round, sb.completed)
+    check_same(a, b, "push-sum")
+    a.close()
+    b.close()
