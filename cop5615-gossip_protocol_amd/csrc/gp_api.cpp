@@ -33,6 +33,8 @@ constexpr uint32_t kSlotMsgMaxActors = 1u << 18;
 // run up to kTileMaxNR rounds per launch
 // (k_ps_tile); GP_FLAG_ONE_ROUND keeps one round per launch.
 constexpr uint32_t kTileMaxActors = 1u << 20;
+constexpr int64_t kMaxBatch = 256;       // rounds per gp_step batch at most
+constexpr size_t kTinyMaxActors = 4096;  // gossip in one workgroup's LDS (k_gs_tiny, <= kTinyActors)
 #ifndef GP_TALLY_THR_DIV
 #define GP_TALLY_THR_DIV 8
 #endif
@@ -232,6 +234,7 @@ struct Handle {
     // small one-GPU line grids: several rounds per launch (k_ps_tile);
     // msg / dir / flags then rotate over kTileBufs buffers, round k's state in [k mod kTileBufs]
     bool tiles = false;
+    bool tiny = false;  // gossip on a tiny graph: a batch of rounds in one workgroup's LDS (k_gs_tiny)
     uint8_t* flg[kTileBufs] = {};
     TileArgs tl{};
     int nbuf() const { return tiles ? (int)kTileBufs : 2; }
@@ -686,6 +689,7 @@ bool fused_marks(const Handle* h) { return kFuseLinkMarks && !h->gossip && !h->g
 const char* round_kernel_name(const Handle* h) {
     // with the receipt tally the timed bracket also holds its passes (the scans, the placement and
     // the per-bucket count, gp_kernels.hip launch_gs_tally), which run after k_gs_full4 every round
+    if (h->tiny) return "k_gs_tiny";
     if (full_quad(h)) return h->tally.cnt ? "k_gs_full4+tally" : "k_gs_full4";
     if (h->gossip && !h->generic) {
         const bool e = gs_pull_early(h->args(0));
@@ -762,6 +766,10 @@ void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed, int piece = 0,
         launch_ps_tile(a, h->tl, nr, h->stream);
         return;
     }
+    if (h->tiny) {
+        launch_gs_tiny(a, nr, h->stream);
+        return;
+    }
     if (h->sharded && !timed) a.work = nullptr;
     Launch l = h->L();
     piece_args(h, piece, a, l);
@@ -832,7 +840,6 @@ constexpr int64_t kTimeGroup = 256;  // = the largest batch: one event pair per 
 #define GP_TAIL_BATCH 32
 #endif
 constexpr int64_t kTailBatch = GP_TAIL_BATCH;  // rounds per batch in a run's tail (0: no tail rule)
-constexpr int64_t kMaxBatch = 256;             // rounds per gp_step batch at most
 
 int ensure_events(Handle* h, int64_t rounds) {
     const size_t need = (size_t)(3 * rounds);
@@ -925,6 +932,7 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
             // tiles: up to kTileMaxNR rounds in one launch, within this batch and timing group
             int nr = 1;
             while (h->tiles && nr < (int)kTileMaxNR && i + nr < B && (i + nr) / every == j) ++nr;
+            if (h->tiny) nr = (int)std::min(B - i, every - i % every);  // the batch (or timing group) at once
             if (group && i % every == 0) HIP_TRY(hipEventRecord(h->kev[3 * j], h->stream));
             if ((rc = launch_round(h, h->next_kernel + i, nullptr, timing && !group && i % every == 0, j, 0, nr)))
                 return rc;
@@ -1897,6 +1905,10 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
         if ((rc = h->alloc(&h->cnt, n, lo)) || (rc = h->alloc(&h->gstate, n, lo))) return bail(rc);
         if (h->generic) {
             if ((rc = h->alloc(&h->inc[0], n, lo)) || (rc = h->alloc(&h->inc[1], n, lo))) return bail(rc);
+            // a tiny graph runs its batches in one workgroup's LDS (k_gs_tiny; GP_FLAG_ONE_ROUND: not)
+            // (up to 4096 actors: 1000 -60%, 5000 -25% .. +4%, 8000 +2%, profiles/round5/tiny/)
+            static_assert(kTinyMaxActors <= kTinyActors, "k_gs_tiny's LDS");
+            h->tiny = !h->sharded && A <= kTinyMaxActors && !(cfg->flags & GP_FLAG_ONE_ROUND);
             // done bitmap and summary (global bit / word numbering): one GPU, the whole graph; a shard
             // holds a replica of every rank's bitmap (its own words current, the others' as of the
             // last exchange), so its senders filter remote targets too

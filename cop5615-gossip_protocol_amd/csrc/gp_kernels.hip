@@ -1664,6 +1664,113 @@ __device__ __forceinline__ void gs_push_body(const RoundArgs& a, const Xchg* xp)
 __global__ __launch_bounds__(kBlock) void k_gs_push(RoundArgs a) { gs_push_body<false>(a, nullptr); }
 
 
+// Gossip on a tiny graph (at most kTinyActors actors, one GPU, the generic path: "full"): the whole
+// run in one workgroup's LDS, nk rounds per launch with workgroup barriers between them.  Iteration
+// k does what the launch F(k) of gs_push_body does: the gate (count after round k - 2), applying
+// round k - 1's receipts (program.fs:97-105), emitting round k (:89-95), with the same draws and
+// filters; the counts go to total[] / the sub-counter ring as F(k)'s gate and block_add leave them.
+// C1 (1000 full gossip): 32 rounds in one launch instead of 32 (profiles/round5/tiny/).
+__global__ __launch_bounds__(kTinyBlock) void k_gs_tiny(RoundArgs a, uint32_t nk) {
+    __shared__ uint32_t s_cnt[kTinyActors], s_inc[kTinyActors];
+    __shared__ uint8_t s_st[kTinyActors];
+    __shared__ uint32_t s_red[kTinyBlock / 64];
+    const uint32_t n = a.g.actors, k0 = a.r, tid = threadIdx.x;
+    for (uint32_t v = tid; v < n; v += kTinyBlock) {
+        s_cnt[v] = a.cnt[v];
+        s_st[v] = a.gstate[v];
+        s_inc[v] = k0 ? a.inc_prev[v] : 0u;  // round k0 - 1's receipts (F(k0) applies them)
+    }
+    // count after round k0 - 2 (F(k0)'s gate)
+    unsigned long long c2 = 0;
+    if (k0 >= 2u) {
+        uint32_t x = tid < 64u ? *part_slot(a.parts, (long long)k0 - 2, tid) : 0u;
+        x = wave_sum(x);  // (wave 0 holds the sum; broadcast below)
+        if (tid == 0) s_red[0] = x;
+        __syncthreads();
+        c2 = (unsigned long long)s_red[0] + (k0 >= 3u ? a.total[k0 - 3u] : 0ull);
+    }
+    __syncthreads();
+    uint32_t k = k0;
+    bool gated = false;
+    for (; k < k0 + nk; ++k) {
+        if (k >= 1u && c2 >= a.target) {  // F(k) exits at its gate, and every later launch too
+            gated = true;
+            break;
+        }
+        if (k >= 2u && tid == 0) a.total[k - 2u] = c2;
+        uint32_t newly = 0;
+        if (k >= 1u) {  // apply round k - 1
+            for (uint32_t v = tid; v < n; v += kTinyBlock) {
+                uint32_t m;
+                if (!generic_deg(a, v, m)) continue;
+                const uint32_t inc = s_inc[v];
+                if (!inc) continue;
+                s_inc[v] = 0u;
+                const uint8_t st = s_st[v];
+                uint32_t tok = st & 3u, done = (st >> 2) & 1u;
+                if (done) continue;
+                const uint32_t c0 = s_cnt[v], c1 = c0 + inc;
+                s_cnt[v] = c1;
+                if (c0 == 0) ++tok;
+                if (c0 <= a.threshold && c1 > a.threshold) {
+                    done = 1;
+                    ++newly;
+                }
+                s_st[v] = (uint8_t)(tok | (done << 2));
+            }
+            newly = wave_sum(newly);
+            if ((tid & 63u) == 0) s_red[tid >> 6] = newly;
+        }
+        __syncthreads();  // round k - 1 applied
+        if (k >= 1u) {
+            uint32_t t = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < kTinyBlock / 64; ++w) t += s_red[w];
+            // round k - 1's sub-counters as F(k)'s block_add leaves them (one slot: the sum)
+            if (tid < 64u) *part_slot(a.parts, (long long)k - 1, tid) = tid == 0 ? t : 0u;
+            c2 = (k >= 2u ? c2 : 0ull) + t;  // now the count after round k - 1
+        }
+        // emit round k (receipts to targets done after round k - 1 are dropped, as the receiver would)
+        for (uint32_t v = tid; v < n; v += kTinyBlock) {
+            uint32_t m;
+            const uint32_t d = generic_deg(a, v, m);
+            if (!d) continue;
+            const uint32_t tok = s_st[v] & 3u;
+            if (!tok) continue;
+            const uint4 px = philox(v, k, kStreamGossip, a.seed);
+            const uint32_t t0 = generic_target(a, v, m, scale_draw(px.x, d));
+            if (!(s_st[t0] & 4u)) atomicAdd(&s_inc[t0], 1u);
+            if (tok > 1u) {
+                const uint32_t t1 = generic_target(a, v, m, scale_draw(px.y, d));
+                if (!(s_st[t1] & 4u)) atomicAdd(&s_inc[t1], 1u);
+            }
+        }
+        __syncthreads();  // round k emitted (s_red free again)
+    }
+    // the state F(k - 1) leaves: counts and states, round k - 1's receipts in inc[(k - 1) & 1] (what
+    // F(k) reads), the other receipt array empty; a gated run also leaves the totals and sub-counters
+    // that the gated launches would (the count stays)
+    uint32_t* inc_last = (k & 1u) ? a.inc_prev : a.inc_cur;  // inc[(k - 1) & 1] (a = args(k0))
+    uint32_t* inc_next = (k & 1u) ? a.inc_cur : a.inc_prev;
+    if ((k0 & 1u) == 0u) {  // args(k0): inc_prev = inc[(k0 - 1) & 1], inc_cur = inc[k0 & 1]
+        uint32_t* x = inc_last;
+        inc_last = inc_next;
+        inc_next = x;
+    }
+    for (uint32_t v = tid; v < n; v += kTinyBlock) {
+        a.cnt[v] = s_cnt[v];
+        a.gstate[v] = s_st[v];
+        inc_last[v] = gated ? 0u : s_inc[v];
+        inc_next[v] = 0u;
+    }
+    if (gated) {
+        for (uint32_t j = k; j < k0 + nk; ++j) {  // launches F(j), j >= k: total[j - 2] = the count
+            if (j >= 2u && tid == 0) a.total[j - 2u] = c2;
+            if (j >= 1u && tid < 64u) *part_slot(a.parts, (long long)j - 1, tid) = 0u;
+        }
+    }
+}
+
 // Full-topology gossip on one GPU (program.fs:89-105, "full" neighbours program.fs:201-206):
 // four consecutive actors per lane, so the per-actor streams (state byte, receipt and count
 // words) are read as one dword / dwordx4 per lane.  Receipts are u32 atomics into inc_cur[t].
@@ -2594,6 +2701,10 @@ uint32_t span_for(uint32_t n, int grid) {
 #define GP_PSQ_PER_CU 7
 #endif
 static int quiet_grid(const Launch& l) { return l.grid < 256 * GP_PSQ_PER_CU ? l.grid : 256 * GP_PSQ_PER_CU; }
+
+void launch_gs_tiny(const RoundArgs& a, int nk, hipStream_t s) {
+    hipLaunchKernelGGL(k_gs_tiny, dim3(1), dim3(kTinyBlock), 0, s, a, (uint32_t)nk);
+}
 
 void launch_ps_tile(const RoundArgs& a, const TileArgs& t, int nr, hipStream_t s) {
     const int boxes = (int)((a.g.actors + kTileSeg - 1) / kTileSeg);

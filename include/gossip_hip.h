@@ -73,8 +73,10 @@ enum gp_flags {
                                   every gp_shard_sync) */
     GP_FLAG_FORCE_PIECES = 2048, /* with GP_FLAG_PIECES: 4 pieces at any size (whole z-planes, or
                                   256 actors on line / 2D, permitting); a test hook, same results */
-    GP_FLAG_ONE_ROUND = 4096,    /* small one-GPU line / 2D / 3D push-sum: one round per launch
-                                  instead of two over boxes of the grid; a test hook, same results */
+    GP_FLAG_ONE_ROUND = 4096,    /* one GPU: one round per launch, also where the library batches
+                                  rounds into one launch (push-sum on small line / 2D grids, gossip
+                                  on graphs of up to 8192 actors through the generic path); a test
+                                  hook, same results */
 };
 
 typedef struct gp_config {

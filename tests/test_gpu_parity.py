@@ -373,3 +373,43 @@ def test_tiles_vs_one_round_c2(topo):
     check_same(a, b, "push-sum")
     a.close()
     b.close()
+
+
+# Gossip on tiny graphs (generic path: "full", or any topology with GP_FLAG_GENERIC; up to 8192
+# actors) runs each batch of rounds in one workgroup's LDS (k_gs_tiny): steps of
+# every length, so a batch can end anywhere, including past convergence.
+TINY_CASES = [
+    (1, "full", 1, False), (2, "full", 2, False), (3, "full", 3, False), (10, "full", 4, False),
+    (100, "full", 5, False), (1000, "full", 6, False), (3000, "full", 7, False), (4095, "full", 8, False),
+    (2000, "line", 9, True), (1000, "3D", 10, True), (3000, "Imp3D", 11, True), (900, "2D", 12, True),
+]
+
+
+@pytest.mark.parametrize("n,topo,seed,generic", TINY_CASES)
+def test_tiny_gossip_vs_oracle(n, topo, seed, generic):
+    gpu, cpu = _pair(n, topo, "gossip", seed, generic=generic, kernel_timing=True)
+    assert gpu.kernel_stats()["kernel"] == "k_gs_tiny"
+    for chunk in (1, 2, 3, 5, 8, 13, 1 << 20):
+        gs, cs = gpu.step(chunk), cpu.step(chunk, threads=8)
+        assert (gs.round, gs.completed, gs.converged) == (cs.round, cs.completed, cs.converged)
+        check_same(gpu, cpu, "gossip")
+        if gs.converged:
+            break
+    gpu.reset()
+    gs = gpu.step()
+    assert (gs.round, gs.completed, gs.converged) == (cs.round, cs.completed, cs.converged)
+    check_same(gpu, cpu, "gossip")
+    gpu.close()
+    cpu.close()
+
+
+def test_tiny_gossip_vs_one_round_c1():
+    """C1 (1000 full gossip) to convergence, one launch per batch against one per round."""
+    a = Simulator(1000, "full", "gossip", seed=1)
+    b = Simulator(1000, "full", "gossip", seed=1, one_round=True, kernel_timing=True)
+    assert b.kernel_stats()["kernel"] != "k_gs_tiny"
+    sa, sb = a.step(), b.step()
+    assert sa.converged and (sa.round, sa.completed) == (sb.round, sb.completed)
+    check_same(a, b, "gossip")
+    a.close()
+    b.close()
