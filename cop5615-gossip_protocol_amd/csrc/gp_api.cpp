@@ -35,6 +35,7 @@ constexpr uint32_t kSlotMsgMaxActors = 1u << 18;
 constexpr uint32_t kTileMaxActors = 1u << 20;
 constexpr int64_t kMaxBatch = 256;       // rounds per gp_step batch at most
 constexpr size_t kTinyMaxActors = 4096;  // gossip in one workgroup's LDS (k_gs_tiny, <= kTinyActors)
+constexpr size_t kTinyGridMaxActors = 3072;  // ... for the grid topologies too (else k_gs_pull)
 #ifndef GP_TALLY_THR_DIV
 #define GP_TALLY_THR_DIV 8
 #endif
@@ -1828,7 +1829,11 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
     h->lay.grid = grid;
     h->gossip = cfg->algo == GP_GOSSIP;
     h->full = cfg->topology == GP_FULL;
-    h->generic = h->full || (cfg->flags & GP_FLAG_GENERIC);
+    // (gossip on a tiny graph of any topology takes the generic path too: k_gs_tiny runs it in LDS; up
+    // to kTinyGridMaxActors, where one workgroup's walk of the actors still beats launches over the
+    // grid kernels, profiles/round5/tiny/)
+    h->generic = h->full || (cfg->flags & GP_FLAG_GENERIC) ||
+                 (h->gossip && !sharded && (size_t)actors <= kTinyGridMaxActors && !(cfg->flags & GP_FLAG_ONE_ROUND));
     h->sharded = sharded;
     h->rank = sharded ? rank : 0;
     h->world = sharded ? world : 1;

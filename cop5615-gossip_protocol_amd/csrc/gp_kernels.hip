@@ -1701,9 +1701,7 @@ __global__ __launch_bounds__(kTinyBlock) void k_gs_tiny(RoundArgs a, uint32_t nk
         uint32_t newly = 0;
         if (k >= 1u) {  // apply round k - 1
             for (uint32_t v = tid; v < n; v += kTinyBlock) {
-                uint32_t m;
-                if (!generic_deg(a, v, m)) continue;
-                const uint32_t inc = s_inc[v];
+                const uint32_t inc = s_inc[v];  // (only actors with neighbours receive)
                 if (!inc) continue;
                 s_inc[v] = 0u;
                 const uint8_t st = s_st[v];
@@ -1732,11 +1730,11 @@ __global__ __launch_bounds__(kTinyBlock) void k_gs_tiny(RoundArgs a, uint32_t nk
         }
         // emit round k (receipts to targets done after round k - 1 are dropped, as the receiver would)
         for (uint32_t v = tid; v < n; v += kTinyBlock) {
+            const uint32_t tok = s_st[v] & 3u;
+            if (!tok) continue;
             uint32_t m;
             const uint32_t d = generic_deg(a, v, m);
             if (!d) continue;
-            const uint32_t tok = s_st[v] & 3u;
-            if (!tok) continue;
             const uint4 px = philox(v, k, kStreamGossip, a.seed);
             const uint32_t t0 = generic_target(a, v, m, scale_draw(px.x, d));
             if (!(s_st[t0] & 4u)) atomicAdd(&s_inc[t0], 1u);

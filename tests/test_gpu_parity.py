@@ -382,6 +382,8 @@ TINY_CASES = [
     (1, "full", 1, False), (2, "full", 2, False), (3, "full", 3, False), (10, "full", 4, False),
     (100, "full", 5, False), (1000, "full", 6, False), (3000, "full", 7, False), (4095, "full", 8, False),
     (2000, "line", 9, True), (1000, "3D", 10, True), (3000, "Imp3D", 11, True), (900, "2D", 12, True),
+    # (the grid topologies take it by default at this size too)
+    (3000, "line", 13, False), (2700, "3D", 14, False), (2500, "Imp3D", 15, False), (2900, "2D", 16, False),
 ]
 
 
@@ -401,6 +403,19 @@ def test_tiny_gossip_vs_oracle(n, topo, seed, generic):
     check_same(gpu, cpu, "gossip")
     gpu.close()
     cpu.close()
+
+
+@pytest.mark.parametrize("n,topo", [(3000, "line"), (2000, "3D"), (3000, "Imp3D")])
+def test_tiny_gossip_grid_vs_one_round(n, topo):
+    """Small grid gossip: the tiny path against the grid kernels (GP_FLAG_ONE_ROUND)."""
+    a = Simulator(n, topo, "gossip", seed=2)
+    b = Simulator(n, topo, "gossip", seed=2, one_round=True, kernel_timing=True)
+    assert b.kernel_stats()["kernel"].startswith("k_gs_pull")
+    sa, sb = a.step(), b.step()
+    assert sa.converged and (sa.round, sa.completed) == (sb.round, sb.completed)
+    check_same(a, b, "gossip")
+    a.close()
+    b.close()
 
 
 def test_tiny_gossip_vs_one_round_c1():
