@@ -690,7 +690,7 @@ bool fused_marks(const Handle* h) { return kFuseLinkMarks && !h->gossip && !h->g
 const char* round_kernel_name(const Handle* h) {
     // with the receipt tally the timed bracket also holds its passes (the scans, the placement and
     // the per-bucket count, gp_kernels.hip launch_gs_tally), which run after k_gs_full4 every round
-    if (h->tiny) return "k_gs_tiny";
+    if (h->tiny) return h->gossip ? "k_gs_tiny" : "k_ps_tiny";
     if (full_quad(h)) return h->tally.cnt ? "k_gs_full4+tally" : "k_gs_full4";
     if (h->gossip && !h->generic) {
         const bool e = gs_pull_early(h->args(0));
@@ -707,6 +707,7 @@ const char* round_kernel_name(const Handle* h) {
 }
 
 const char* aux_kernel_name(const Handle* h) {
+    if (h->tiny) return "";
     if (h->generic) return h->gossip ? (h->sharded && h->world > 1 ? "k_shard_done_out" : "") : "k_scan_* + k_ps_push_fill";
     if (!h->g.has_link || fused_marks(h)) return "";
     if (h->sharded) return h->gossip ? "k_gs_link_scatter_x" : "k_ps_link_scatter_x";
@@ -768,7 +769,8 @@ void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed, int piece = 0,
         return;
     }
     if (h->tiny) {
-        launch_gs_tiny(a, nr, h->stream);
+        if (h->gossip) launch_gs_tiny(a, nr, h->stream);
+        else launch_ps_tiny(a, nr, h->stream);
         return;
     }
     if (h->sharded && !timed) a.work = nullptr;
@@ -808,6 +810,7 @@ int launch_aux(Handle* h, int64_t k, const Xchg* x, int piece = 0) {
     Launch l = h->L();
     piece_args(h, piece, a, l);
     int rc;
+    if (h->tiny) return GP_OK;  // (k_ps_tiny builds its buckets itself)
     // (a shard clears before its round kernel: its tail rounds write their own link marks)
     if (!fused_marks(h) && !h->sharded && (rc = clear_tags_if_due(h, r))) return rc;
     (void)rc;
@@ -933,7 +936,8 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
             // tiles: up to kTileMaxNR rounds in one launch, within this batch and timing group
             int nr = 1;
             while (h->tiles && nr < (int)kTileMaxNR && i + nr < B && (i + nr) / every == j) ++nr;
-            if (h->tiny) nr = (int)std::min(B - i, every - i % every);  // the batch (or timing group) at once
+            // tiny: the batch at once (with kernel timing: its timing group)
+            if (h->tiny) nr = (int)(timing ? std::min(B - i, every - i % every) : B - i);
             if (group && i % every == 0) HIP_TRY(hipEventRecord(h->kev[3 * j], h->stream));
             if ((rc = launch_round(h, h->next_kernel + i, nullptr, timing && !group && i % every == 0, j, 0, nr)))
                 return rc;
@@ -1832,8 +1836,11 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
     // (gossip on a tiny graph of any topology takes the generic path too: k_gs_tiny runs it in LDS; up
     // to kTinyGridMaxActors, where one workgroup's walk of the actors still beats launches over the
     // grid kernels, profiles/round5/tiny/)
+    // ... and push-sum on a tiny Imp3D graph (k_ps_tiny; the other grids keep their faster kernels)
+    const bool one_round = (cfg->flags & GP_FLAG_ONE_ROUND) != 0;
     h->generic = h->full || (cfg->flags & GP_FLAG_GENERIC) ||
-                 (h->gossip && !sharded && (size_t)actors <= kTinyGridMaxActors && !(cfg->flags & GP_FLAG_ONE_ROUND));
+                 (h->gossip && !sharded && (size_t)actors <= kTinyGridMaxActors && !one_round) ||
+                 (!h->gossip && cfg->topology == GP_IMP3D && !sharded && actors <= kTinyPsActors && !one_round);
     h->sharded = sharded;
     h->rank = sharded ? rank : 0;
     h->world = sharded ? world : 1;
@@ -1977,6 +1984,8 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
                 if ((rc = h->alloc(&h->bcnt[i], A)) || (rc = h->alloc(&h->boff[i], A + 1)) ||
                     (rc = h->alloc(&h->slot[i], A)))
                     return bail(rc);
+            // a tiny graph runs its batches in one workgroup's LDS (k_ps_tiny; GP_FLAG_ONE_ROUND: not)
+            h->tiny = !h->sharded && A <= kTinyPsActors && !(cfg->flags & GP_FLAG_ONE_ROUND);
             if ((rc = h->alloc(&h->tgt, A)) || (rc = h->alloc(&h->pos, A)) ||
                 (rc = h->alloc(&h->scan_scratch, scan_scratch_words((uint32_t)A))))
                 return bail(rc);

@@ -264,6 +264,9 @@ void launch_ps_tile(const RoundArgs& a, const TileArgs& t, int nr, hipStream_t s
 // Gossip on tiny graphs (generic path, one GPU): nk rounds F(r) .. F(r + nk - 1) in one workgroup's LDS
 constexpr uint32_t kTinyActors = 8192, kTinyBlock = 1024;
 void launch_gs_tiny(const RoundArgs& a, int nk, hipStream_t s);
+// ... and push-sum (generic path): the buckets by destination rebuilt in LDS every round
+constexpr uint32_t kTinyPsActors = 2048;
+void launch_ps_tiny(const RoundArgs& a, int nk, hipStream_t s);
 void launch_gs_pull(const RoundArgs& a, const Launch& l);
 // Gossip grid rounds on graphs below 2^18 actors (one GPU) issue their level-1 loads ahead of
 // the gate: k_gs_pull<LINK, true>.  (At 1M actors the unconditional loads cost more than the

@@ -1769,6 +1769,144 @@ __global__ __launch_bounds__(kTinyBlock) void k_gs_tiny(RoundArgs a, uint32_t nk
     }
 }
 
+// Push-sum on a tiny graph (at most kTinyPsActors actors, one GPU, the generic path), a batch of
+// rounds in one workgroup's LDS: iteration k does what k_ps_push_emit + the bucket scan + fill do for
+// F(k): the gate (count after round k - 1), each actor's collect of round k - 1's messages in
+// ascending source order (program.fs:119-143, the same selection walk), its update and emission with
+// the same draw, then round k's buckets by destination (LDS counts, a block scan, positions), so the
+// next iteration's receivers find their senders.  Totals and sub-counters as F(k) leaves them.
+__device__ __forceinline__ void tiny_buckets(uint32_t n, const uint32_t* tgt, uint32_t* cnt, uint32_t* off,
+                                             uint32_t* pos, uint32_t* slot, uint32_t* wsum) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    for (uint32_t v = tid; v < n; v += kTinyBlock) cnt[v] = 0u;
+    __syncthreads();
+    for (uint32_t v = tid; v < n; v += kTinyBlock)
+        if (tgt[v] != 0xFFFFFFFFu) pos[v] = atomicAdd(&cnt[tgt[v]], 1u);
+    __syncthreads();
+    // exclusive scan of cnt[0 .. n): two entries per thread, a wave scan, the waves' totals
+    static_assert(2u * kTinyBlock >= kTinyPsActors, "two entries per thread");
+    const uint32_t i0 = 2u * tid, i1 = i0 + 1u;
+    const uint32_t a0 = i0 < n ? cnt[i0] : 0u, a1 = i1 < n ? cnt[i1] : 0u;
+    uint32_t inc = a0 + a1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63u) wsum[w] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t j = 0; j < w; ++j) base += wsum[j];
+    const uint32_t ex = base + inc - a0 - a1;
+    if (i0 < n) off[i0] = ex;
+    if (i1 < n) off[i1] = ex + a0;
+    __syncthreads();
+    for (uint32_t v = tid; v < n; v += kTinyBlock)
+        if (tgt[v] != 0xFFFFFFFFu) slot[off[tgt[v]] + pos[v]] = v;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kTinyBlock) void k_ps_tiny(RoundArgs a, uint32_t nk) {
+    __shared__ double2 s_msg[2][kTinyPsActors];  // round k - 1's messages, round k's
+    __shared__ uint32_t s_tgt[kTinyPsActors], s_cnt[kTinyPsActors], s_off[kTinyPsActors], s_pos[kTinyPsActors],
+        s_slot[kTinyPsActors];
+    __shared__ uint8_t s_flg[kTinyPsActors];
+    __shared__ uint32_t s_red[kTinyBlock / 64];
+    const uint32_t n = a.g.actors, k0 = a.r, tid = threadIdx.x;
+    for (uint32_t v = tid; v < n; v += kTinyBlock) {
+        s_flg[v] = a.flags[v];
+        s_tgt[v] = k0 ? a.tgt_cur[v] : 0xFFFFFFFFu;  // round k0 - 1's targets (tgt is one array)
+        s_msg[0][v] = k0 ? a.msg_prev[v] : make_double2(0.0, 0.0);
+    }
+    // count after round k0 - 1 (F(k0)'s gate)
+    unsigned long long c1 = 0;
+    if (k0 >= 1u) {
+        uint32_t x = tid < 64u ? *part_slot(a.parts, (long long)k0 - 1, tid) : 0u;
+        x = wave_sum(x);
+        if (tid == 0) s_red[0] = x;
+        __syncthreads();
+        c1 = (unsigned long long)s_red[0] + (k0 >= 2u ? a.total[k0 - 2u] : 0ull);
+    }
+    __syncthreads();
+    tiny_buckets(n, s_tgt, s_cnt, s_off, s_pos, s_slot, s_red);
+    uint32_t k = k0, in = 0;
+    bool gated = false;
+    for (; k < k0 + nk; ++k, in ^= 1u) {
+        if (c1 >= a.target) {  // F(k) exits at its gate, and every later launch too
+            gated = true;
+            break;
+        }
+        if (k >= 1u && tid == 0) a.total[k - 1u] = c1;
+        uint32_t newly = 0;
+        for (uint32_t v = tid; v < n; v += kTinyBlock) {
+            uint32_t m;
+            const uint32_t d = generic_deg(a, v, m);
+            uint32_t t = 0xFFFFFFFFu;
+            if (d) {
+                uint8_t f = s_flg[v];
+                double ss = 0.0, ww = 0.0;
+                uint32_t cin = 0;
+                if (k) {
+                    const uint32_t c = s_cnt[v], o = s_off[v];
+                    long long last = -1;
+                    for (uint32_t i = 0; i < c; ++i) {  // ascending source id (k_ps_push_emit's walk)
+                        uint32_t best = 0xFFFFFFFFu;
+                        for (uint32_t j = 0; j < c; ++j) {
+                            const uint32_t sj = s_slot[o + j];
+                            if ((long long)sj > last && sj < best) best = sj;
+                        }
+                        const double2 mm = s_msg[in][best];
+                        ss += mm.x;
+                        ww += mm.y;
+                        last = best;
+                    }
+                    cin = c;
+                }
+                double2 held = make_double2(0.0, 0.0);
+                if (!(f & 16u)) held = k ? s_msg[in][v] : make_double2((double)v, 1.0);
+                const PsOut o = ps_update(f, held, ss, ww, cin, a.delta, a.term_limit);
+                if (o.send) {
+                    const uint4 x = philox(v, k, kStreamPush, a.seed);
+                    t = generic_target(a, v, m, scale_draw(x.x, d));
+                    s_msg[in ^ 1u][v] = o.msg;
+                }
+                s_flg[v] = f;
+                if (o.conv_now) {
+                    a.frozen[v] = o.msg;
+                    ++newly;
+                }
+            }
+            s_tgt[v] = t;
+        }
+        newly = wave_sum(newly);
+        if ((tid & 63u) == 0) s_red[tid >> 6] = newly;
+        __syncthreads();  // round k collected and emitted
+        uint32_t tsum = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kTinyBlock / 64; ++w) tsum += s_red[w];
+        if (tid < 64u) *part_slot(a.parts, (long long)k, tid) = tid == 0 ? tsum : 0u;
+        c1 += tsum;  // now the count after round k
+        __syncthreads();  // (s_red read)
+        tiny_buckets(n, s_tgt, s_cnt, s_off, s_pos, s_slot, s_red);
+    }
+    // the state F(k - 1) leaves: flags, round k - 1's messages in msg[(k - 1) & 1] and their targets
+    // (a = args(k0); msg_prev is the other buffer of the pair, read-only in the per-round kernels)
+    double2* out = ((k - 1u) & 1u) == (k0 & 1u) ? a.msg_cur : const_cast<double2*>(a.msg_prev);
+    for (uint32_t v = tid; v < n; v += kTinyBlock) {
+        a.flags[v] = s_flg[v];
+        if (k > k0) {
+            a.tgt_cur[v] = s_tgt[v];
+            if (s_tgt[v] != 0xFFFFFFFFu) out[v] = s_msg[in][v];
+        }
+    }
+    if (gated) {
+        for (uint32_t j = k; j < k0 + nk; ++j) {  // launches F(j), j >= k: total[j - 1] = the count
+            if (j >= 1u && tid == 0) a.total[j - 1u] = c1;
+            if (tid < 64u) *part_slot(a.parts, (long long)j, tid) = 0u;
+        }
+    }
+}
+
 // Full-topology gossip on one GPU (program.fs:89-105, "full" neighbours program.fs:201-206):
 // four consecutive actors per lane, so the per-actor streams (state byte, receipt and count
 // words) are read as one dword / dwordx4 per lane.  Receipts are u32 atomics into inc_cur[t].
@@ -2699,6 +2837,10 @@ uint32_t span_for(uint32_t n, int grid) {
 #define GP_PSQ_PER_CU 7
 #endif
 static int quiet_grid(const Launch& l) { return l.grid < 256 * GP_PSQ_PER_CU ? l.grid : 256 * GP_PSQ_PER_CU; }
+
+void launch_ps_tiny(const RoundArgs& a, int nk, hipStream_t s) {
+    hipLaunchKernelGGL(k_ps_tiny, dim3(1), dim3(kTinyBlock), 0, s, a, (uint32_t)nk);
+}
 
 void launch_gs_tiny(const RoundArgs& a, int nk, hipStream_t s) {
     hipLaunchKernelGGL(k_gs_tiny, dim3(1), dim3(kTinyBlock), 0, s, a, (uint32_t)nk);

@@ -428,3 +428,46 @@ def test_tiny_gossip_vs_one_round_c1():
     check_same(a, b, "gossip")
     a.close()
     b.close()
+
+
+# Push-sum on tiny graphs through the generic path ("full", or GP_FLAG_GENERIC; up to 2048 actors):
+# a batch of rounds in one workgroup's LDS, the buckets by destination rebuilt there every round
+# (k_ps_tiny).
+TINY_PS_CASES = [
+    (1, "full", 1, False), (2, "full", 2, False), (3, "full", 3, False), (39, "full", 4, False),
+    (200, "full", 5, False), (1000, "full", 6, False), (2047, "full", 7, False),
+    (1000, "Imp3D", 8, True), (1000, "3D", 9, True), (500, "line", 10, True), (900, "2D", 11, True),
+    (1000, "Imp3D", 12, False), (2000, "Imp3D", 13, False),  # (Imp3D takes it by default at this size)
+]
+
+
+@pytest.mark.parametrize("n,topo,seed,generic", TINY_PS_CASES)
+def test_tiny_pushsum_vs_oracle(n, topo, seed, generic):
+    gpu, cpu = _pair(n, topo, "push-sum", seed, generic=generic, kernel_timing=True)
+    assert gpu.kernel_stats()["kernel"] == "k_ps_tiny"
+    for chunk in (1, 2, 3, 5, 8, 13, 1 << 20):
+        gs, cs = gpu.step(chunk), cpu.step(chunk, threads=8)
+        assert (gs.round, gs.completed, gs.converged) == (cs.round, cs.completed, cs.converged)
+        check_same(gpu, cpu, "push-sum")
+        if gs.converged:
+            break
+    assert gs.converged
+    assert gs.sum_s == pytest.approx(cs.sum_s, rel=1e-12) and gs.sum_w == pytest.approx(cs.sum_w, rel=1e-12)
+    gpu.reset()
+    gs = gpu.step()
+    assert (gs.round, gs.completed, gs.converged) == (cs.round, cs.completed, cs.converged)
+    check_same(gpu, cpu, "push-sum")
+    gpu.close()
+    cpu.close()
+
+
+def test_tiny_pushsum_vs_one_round():
+    """`1000 full push-sum` to convergence, one launch per batch against the per-round passes."""
+    a = Simulator(1000, "full", "push-sum", seed=3)
+    b = Simulator(1000, "full", "push-sum", seed=3, one_round=True, kernel_timing=True)
+    assert b.kernel_stats()["kernel"] == "k_ps_push_emit"
+    sa, sb = a.step(), b.step()
+    assert sa.converged and (sa.round, sa.completed) == (sb.round, sb.completed)
+    check_same(a, b, "push-sum")
+    a.close()
+    b.close()
