@@ -34,7 +34,7 @@ constexpr uint32_t kSlotMsgMaxActors = 1u << 18;
 // (k_ps_tile); GP_FLAG_ONE_ROUND keeps one round per launch.
 constexpr uint32_t kTileMaxActors = 1u << 20;
 constexpr int64_t kMaxBatch = 256;       // rounds per gp_step batch at most
-constexpr size_t kTinyMaxActors = 4096;  // gossip in one workgroup's LDS (k_gs_tiny, <= kTinyActors)
+constexpr size_t kTinyMaxActors = 8192;  // gossip in one workgroup's LDS (k_gs_tiny, <= kTinyActors)
 constexpr size_t kTinyGridMaxActors = 3072;  // ... for the grid topologies too (else k_gs_pull)
 #ifndef GP_TALLY_THR_DIV
 #define GP_TALLY_THR_DIV 8
@@ -1920,7 +1920,7 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
         if (h->generic) {
             if ((rc = h->alloc(&h->inc[0], n, lo)) || (rc = h->alloc(&h->inc[1], n, lo))) return bail(rc);
             // a tiny graph runs its batches in one workgroup's LDS (k_gs_tiny; GP_FLAG_ONE_ROUND: not)
-            // (up to 4096 actors: 1000 -60%, 5000 -25% .. +4%, 8000 +2%, profiles/round5/tiny/)
+            // (up to 8192 actors, the LDS capacity: 1000 -67%, 5000 -36%, 8191 -12%, profiles/round5/tiny/)
             static_assert(kTinyMaxActors <= kTinyActors, "k_gs_tiny's LDS");
             h->tiny = !h->sharded && A <= kTinyMaxActors && !(cfg->flags & GP_FLAG_ONE_ROUND);
             // done bitmap and summary (global bit / word numbering): one GPU, the whole graph; a shard

@@ -380,7 +380,7 @@ def test_tiles_vs_one_round_c2(topo):
 # every length, so a batch can end anywhere, including past convergence.
 TINY_CASES = [
     (1, "full", 1, False), (2, "full", 2, False), (3, "full", 3, False), (10, "full", 4, False),
-    (100, "full", 5, False), (1000, "full", 6, False), (3000, "full", 7, False), (4095, "full", 8, False),
+    (100, "full", 5, False), (1000, "full", 6, False), (3000, "full", 7, False), (4095, "full", 8, False), (8191, "full", 17, False),
     (2000, "line", 9, True), (1000, "3D", 10, True), (3000, "Imp3D", 11, True), (900, "2D", 12, True),
     # (the grid topologies take it by default at this size too)
     (3000, "line", 13, False), (2700, "3D", 14, False), (2500, "Imp3D", 15, False), (2900, "2D", 16, False),
