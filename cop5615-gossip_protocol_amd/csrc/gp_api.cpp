@@ -35,7 +35,7 @@ constexpr uint32_t kSlotMsgMaxActors = 1u << 18;
 constexpr uint32_t kTileMaxActors = 1u << 20;
 constexpr int64_t kMaxBatch = 256;       // rounds per gp_step batch at most
 constexpr size_t kTinyMaxActors = 8192;  // gossip in one workgroup's LDS (k_gs_tiny, <= kTinyActors)
-constexpr size_t kTinyGridMaxActors = 3072;  // ... for the grid topologies too (else k_gs_pull)
+constexpr size_t kTinyGridMaxActors = 4096;  // ... for the grid topologies too (else k_gs_pull)
 #ifndef GP_TALLY_THR_DIV
 #define GP_TALLY_THR_DIV 8
 #endif
@@ -1836,8 +1836,8 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
     h->gossip = cfg->algo == GP_GOSSIP;
     h->full = cfg->topology == GP_FULL;
     // (gossip on a tiny graph of any topology takes the generic path too: k_gs_tiny runs it in LDS; up
-    // to kTinyGridMaxActors, where one workgroup's walk of the actors still beats launches over the
-    // grid kernels, profiles/round5/tiny/)
+    // to kTinyGridMaxActors, where one workgroup's walk of the actors still beats launches of the grid
+    // kernels: 4000 3D -22%, 8000 3D +55%, profiles/round5/tiny/)
     // ... and push-sum on a tiny Imp3D graph (k_ps_tiny; the other grids keep their faster kernels)
     const bool one_round = (cfg->flags & GP_FLAG_ONE_ROUND) != 0;
     h->generic = h->full || (cfg->flags & GP_FLAG_GENERIC) ||

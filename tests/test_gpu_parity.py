@@ -384,6 +384,7 @@ TINY_CASES = [
     (2000, "line", 9, True), (1000, "3D", 10, True), (3000, "Imp3D", 11, True), (900, "2D", 12, True),
     # (the grid topologies take it by default at this size too)
     (3000, "line", 13, False), (2700, "3D", 14, False), (2500, "Imp3D", 15, False), (2900, "2D", 16, False),
+    (3900, "2D", 18, False), (4000, "3D", 19, False),
 ]
 
 
