@@ -1775,11 +1775,14 @@ __global__ __launch_bounds__(kTinyBlock) void k_gs_tiny(RoundArgs a, uint32_t nk
 // ascending source order (program.fs:119-143, the same selection walk), its update and emission with
 // the same draw, then round k's buckets by destination (LDS counts, a block scan, positions), so the
 // next iteration's receivers find their senders.  Totals and sub-counters as F(k) leaves them.
+// (zero: cnt is not all zero yet; the round loop zeroes each receiver's count as it reads it)
 __device__ __forceinline__ void tiny_buckets(uint32_t n, const uint32_t* tgt, uint32_t* cnt, uint32_t* off,
-                                             uint32_t* pos, uint32_t* slot, uint32_t* wsum) {
+                                             uint32_t* pos, uint32_t* slot, uint32_t* wsum, bool zero) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-    for (uint32_t v = tid; v < n; v += kTinyBlock) cnt[v] = 0u;
-    __syncthreads();
+    if (zero) {
+        for (uint32_t v = tid; v < n; v += kTinyBlock) cnt[v] = 0u;
+        __syncthreads();
+    }
     for (uint32_t v = tid; v < n; v += kTinyBlock)
         if (tgt[v] != 0xFFFFFFFFu) pos[v] = atomicAdd(&cnt[tgt[v]], 1u);
     __syncthreads();
@@ -1828,7 +1831,7 @@ __global__ __launch_bounds__(kTinyBlock) void k_ps_tiny(RoundArgs a, uint32_t nk
         c1 = (unsigned long long)s_red[0] + (k0 >= 2u ? a.total[k0 - 2u] : 0ull);
     }
     __syncthreads();
-    tiny_buckets(n, s_tgt, s_cnt, s_off, s_pos, s_slot, s_red);
+    tiny_buckets(n, s_tgt, s_cnt, s_off, s_pos, s_slot, s_red, true);
     uint32_t k = k0, in = 0;
     bool gated = false;
     for (; k < k0 + nk; ++k, in ^= 1u) {
@@ -1841,13 +1844,15 @@ __global__ __launch_bounds__(kTinyBlock) void k_ps_tiny(RoundArgs a, uint32_t nk
         for (uint32_t v = tid; v < n; v += kTinyBlock) {
             uint32_t m;
             const uint32_t d = generic_deg(a, v, m);
+            const uint32_t c = s_cnt[v];
+            s_cnt[v] = 0u;  // (read by v only; round k's counts start from zero)
             uint32_t t = 0xFFFFFFFFu;
             if (d) {
                 uint8_t f = s_flg[v];
                 double ss = 0.0, ww = 0.0;
                 uint32_t cin = 0;
                 if (k) {
-                    const uint32_t c = s_cnt[v], o = s_off[v];
+                    const uint32_t o = s_off[v];
                     long long last = -1;
                     for (uint32_t i = 0; i < c; ++i) {  // ascending source id (k_ps_push_emit's walk)
                         uint32_t best = 0xFFFFFFFFu;
@@ -1887,7 +1892,7 @@ __global__ __launch_bounds__(kTinyBlock) void k_ps_tiny(RoundArgs a, uint32_t nk
         if (tid < 64u) *part_slot(a.parts, (long long)k, tid) = tid == 0 ? tsum : 0u;
         c1 += tsum;  // now the count after round k
         __syncthreads();  // (s_red read)
-        tiny_buckets(n, s_tgt, s_cnt, s_off, s_pos, s_slot, s_red);
+        tiny_buckets(n, s_tgt, s_cnt, s_off, s_pos, s_slot, s_red, false);
     }
     // the state F(k - 1) leaves: flags, round k - 1's messages in msg[(k - 1) & 1] and their targets
     // (a = args(k0); msg_prev is the other buffer of the pair, read-only in the per-round kernels)
