@@ -2768,13 +2768,19 @@ __global__ void k_fill_u8(uint8_t* p, uint8_t val, size_t n) {
 
 // total[a] from the round-a sub-counters; with `out`, also total[first .. a] into out[0 ..
 // a - first] (host-mapped memory: the host reads the batch's counts without a copy).
+// total[b0 .. a] from the sub-counters (b0 < a: the rounds of the last launch of a batch that ran
+// several, k_ps_tile), one wave, the running count carried in registers
 __global__ void k_finalize(unsigned long long* total, uint32_t* parts, long long a, unsigned long long* out,
-                           long long first) {
-    unsigned long long x = *part_slot(parts, a, threadIdx.x);
+                           long long first, long long b0) {
+    unsigned long long x = b0 >= 1 ? total[b0 - 1] : 0ull;
+    for (long long b = b0; b <= a; ++b) {
+        unsigned long long y = *part_slot(parts, b, threadIdx.x);
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-    x += a >= 1 ? total[a - 1] : 0ull;
-    if (threadIdx.x == 0) total[a] = x;
+        for (int off = 32; off > 0; off >>= 1) y += __shfl_xor(y, off, 64);
+        x += y;
+        if (threadIdx.x == 0) total[b] = x;
+    }
+    if (b0 < a) __threadfence();  // (lane 0's totals, read back below by other lanes)
     if (out)
         for (long long i = threadIdx.x; first + i <= a; i += 64) out[i] = first + i == a ? x : total[first + i];
 }
@@ -3059,10 +3065,9 @@ void launch_fill_u8(uint8_t* p, uint8_t v, size_t n, hipStream_t s) {
 
 void launch_finalize(unsigned long long* total, uint32_t* parts, long long a, hipStream_t s, unsigned long long* out,
                      long long first, bool pairs) {
-    if (pairs)  // the last launch's earlier rounds have no total yet
-        for (long long b = std::max(a - (long long)kTileMaxNR + 1, 0ll); b < a; ++b)
-            hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, total, parts, b, nullptr, 0ll);
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, total, parts, a, out, first);
+    // (pairs: the last launch's earlier rounds have no total yet either)
+    const long long b0 = pairs ? std::max(a - (long long)kTileMaxNR + 1, 0ll) : a;
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, total, parts, a, out, first, b0);
 }
 
 void launch_ps_init(uint8_t* flags, const Geom& g, uint32_t lo, uint32_t hi, uint32_t full, uint32_t term_init,
