@@ -644,7 +644,7 @@ int reset(Handle* h) {
     h->converged = false;
     // (tiny: the whole batch is one launch, and its rounds past convergence exit in the kernel, so
     // the largest batch from the start: one host sync for C1)
-    h->batch = h->tiny ? kMaxBatch : 8;
+    h->batch = h->tiny || h->tiles ? kMaxBatch : 8;
     h->awaiting_deliver = false;
     h->piece_next = 0;
     h->round_slot = -1;
@@ -1000,7 +1000,7 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         // completed no node doubles again (a long quiet tail, e.g. line gossip, would otherwise
         // pay a host sync every GP_TAIL_BATCH rounds).
         const bool tail = kTailBatch > 0 && h->completed * 32 >= h->lay.nodes * 31;
-        if (!tail || h->tiny) h->batch = std::min<int64_t>(h->batch * 2, kMaxBatch);
+        if (!tail || h->tiny || h->tiles) h->batch = std::min<int64_t>(h->batch * 2, kMaxBatch);
         else if (!was_tail || h->completed != before) h->batch = kTailBatch;
         else h->batch = std::min<int64_t>(h->batch * 2, kMaxBatch);
     }
