@@ -345,8 +345,17 @@ def main_group(args):
     elapsed = time.perf_counter() - t0
     progress(0, f"{args.steps} timed step(s): {elapsed * 1e3:.1f} ms")
     ks = eng.kernel_stats()
-    per_rank = {"actors": own, "world": N, "round_kernel_ms": ks["avg_ms"], "aux_kernel_ms": ks["aux_avg_ms"],
-                "kernel": ks["kernel"], "aux_kernel": ks["aux_kernel"], "sampled_rounds": ks["launches"]}
+    per_rank = {"actors": own, "world": N, "kernel": ks["kernel"], "aux_kernel": ks["aux_kernel"],
+                "sampled_rounds": ks["launches"]}
+    if args.one_device:
+        # rank 0's hipEvents sit on a stream that shares the one device with every other shard's
+        # kernels, so they bracket the other shards' work too: not a per-rank time
+        per_rank.update(round_kernel_ms_device_shared=ks["avg_ms"], aux_kernel_ms_device_shared=ks["aux_avg_ms"],
+                        timing_note="--one-device: rank 0's events bracket all shards' kernels on the shared "
+                                    "device; per-rank kernel times come from a kernel trace "
+                                    "(tools/shard_loopback_prof.py)")
+    else:
+        per_rank.update(round_kernel_ms=ks["avg_ms"], aux_kernel_ms=ks["aux_avg_ms"])
     transport = ("device copies on one GPU (GP_FLAG_ONE_DEVICE: the multi-GPU code path, no RCCL)"
                  if args.one_device else "RCCL ncclCommInitAll + grouped ncclSend/ncclRecv")
     out = emit_line(args, name=name, n_arg=n_arg, topology=topology, algorithm=algorithm, window=window,

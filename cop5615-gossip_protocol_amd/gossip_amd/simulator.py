@@ -39,7 +39,7 @@ class Simulator:
         graph size (a test hook; it is on by default from 2^20 actors); tally_fallbacks: the receipt
         tally's counted-batch placement and 32-bit receipt escape everywhere (a test hook);
         force_pieces: num_gpus > 1, rounds in 4 pieces at any size (a test hook; the group runs
-        them from 2^20 actors per shard)."""
+        them from 2^25 actors per shard)."""
         if topology not in _abi.TOPOLOGIES:
             raise ValueError(f"unknown topology {topology!r} (case-sensitive: {list(_abi.TOPOLOGIES)})")
         if algorithm not in _abi.ALGOS:

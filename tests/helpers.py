@@ -127,14 +127,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def run_dist_job(world, backend, n, topology, algorithm, seed, cap, timeout):
-    """Launch tests/dist_shard_job.py under torch.distributed.run with `world` ranks; returns the
-    rank parts (status, trace, state arrays) in rank order."""
+def run_dist_job(world, backend, n, topology, algorithm, seed, cap, timeout, extra=()):
+    """Launch tests/dist_shard_job.py under torch.distributed.run with `world` ranks (extra: more job
+    options, e.g. --force-pieces); returns the rank parts (status, trace, state arrays, shard counters)
+    in rank order."""
     out = tempfile.mkdtemp(prefix="gp_dist_")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_shard_job.py"), "--backend", backend, "--n-arg", str(n),
-           "--topology", topology, "--algorithm", algorithm, "--seed", str(seed), "--cap", str(cap), "--out", out]
+           "--topology", topology, "--algorithm", algorithm, "--seed", str(seed), "--cap", str(cap or 0), "--out", out,
+           *extra]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]

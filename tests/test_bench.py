@@ -51,7 +51,7 @@ def test_bench_group_one_device(capsys):
     assert line["config"]["rounds_per_step"] == 20
     pr = line["per_rank"]
     assert pr["world"] == 4 and 0 < pr["actors"] < line["config"]["actors"]
-    assert pr["round_kernel_ms"] > 0
+    assert pr["round_kernel_ms_device_shared"] > 0 and "round_kernel_ms" not in pr  # one device: not per rank
     base = line["strong_scaling_base"]
     assert base["rounds_per_step"] == 20 and base["value"] > 0
     assert base["t1_over_n_tn"] == pytest.approx(line["value"] / (4 * base["value"]))

@@ -323,9 +323,9 @@ def test_full_gossip_tally_fallbacks_vs_oracle(n, seed, forced):
     cpu.close()
 
 
-# Small one-GPU line grids (line, 2D) run two rounds per launch (k_ps_tile): batches
-# of every parity, so that pairs and single rounds alternate and a step can end after either round
-# of a pair; segment edges, the line's ends and tiny graphs.
+# Small one-GPU line grids (line, 2D) run up to 8 rounds per launch (k_ps_tile): batches
+# of every length, so that launches of 1 .. 8 rounds alternate and a step can end after any round of a
+# launch; segment edges, the line's ends and tiny graphs.
 TILE_CASES = [
     (1, "line", 1, None), (2, "line", 1, None), (3, "line", 2, None), (9, "2D", 3, None), (253, "line", 4, None),
     (254, "2D", 5, None), (1000, "line", 6, None), (5000, "2D", 7, None), (20000, "line", 9, 1500),
@@ -353,7 +353,7 @@ def test_tiles_vs_oracle(n, topo, seed, cap):
     if cap is None:
         assert gs.converged
     assert gs.sum_s == pytest.approx(cs.sum_s, rel=1e-12) and gs.sum_w == pytest.approx(cs.sum_w, rel=1e-12)
-    gpu.reset()  # a second run: the three state buffers start clean
+    gpu.reset()  # a second run: the 9 state buffers (kTileBufs) start clean
     gs2 = gpu.step(cs.round)
     assert (gs2.round, gs2.completed) == (cs.round, cs.completed)
     check_same(gpu, cpu, "push-sum")
@@ -363,7 +363,7 @@ def test_tiles_vs_oracle(n, topo, seed, cap):
 
 @pytest.mark.parametrize("topo", ["line", "2D"])
 def test_tiles_vs_one_round_c2(topo):
-    """C2 line / 2D to convergence (1481 rounds): two rounds per launch against one round per
+    """C2 line / 2D to convergence (1481 rounds): up to 8 rounds per launch against one round per
     launch (GP_FLAG_ONE_ROUND, pinned by the oracle above and by the fingerprints)."""
     a = Simulator(100000, topo, "push-sum", seed=1)
     b = Simulator(100000, topo, "push-sum", seed=1, one_round=True, kernel_timing=True)

@@ -34,9 +34,15 @@ kt() {  # $1 = output name, rest = command
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 ${KT_TIMEOUT:-240} rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$n" -o kt -- "$@" > "$O/$n.log" 2>&1 )
   rc=$?; echo "kt $n rc=$rc"; tail -1 "$O/$n.log"; [ $rc -eq 0 ] || return $rc
   python3 "$R/tools/kt_summary.py" "$O/$n/kt_kernel_trace.csv" > "$O/$n.summary" && head -n ${KT_LINES:-6} "$O/$n.summary" || return $?
-  # KT_POST: a command run on the trace before it is dropped (KT_DROP=1: the trace CSV is too big to
-  # travel back, gpurun merges 64 MiB at most)
-  if [ -n "$KT_POST" ]; then eval "$KT_POST" > "$O/$n.post" 2>&1; cat "$O/$n.post"; fi
+  # KT_POST (dev-only): the name of one post-processing script of tools/ run on the trace before it is
+  # dropped (KT_DROP=1: the trace CSV is too big to travel back, gpurun merges 64 MiB at most); only
+  # the names below are accepted, nothing from the environment is evaluated
+  case "${KT_POST:-}" in
+    "") ;;
+    trace_overlap|trace_gaps|loop_phase_kernels|kt_round_series)
+      python3 "$R/tools/$KT_POST.py" "$O/$n/kt_kernel_trace.csv" ${KT_POST_ARGS} > "$O/$n.post" 2>&1; cat "$O/$n.post" ;;
+    *) echo "KT_POST=$KT_POST: not one of trace_overlap, trace_gaps, loop_phase_kernels, kt_round_series"; return 2 ;;
+  esac
   if [ "${KT_DROP:-0}" = 1 ]; then rm -f "$O/$n/kt_kernel_trace.csv"; fi
 }
 case $MODE in
