@@ -368,9 +368,7 @@ __device__ __forceinline__ PsLevel1 ps_level1(const RoundArgs& a, const Geom& g,
         if (PRE) p.held = a.msg_prev[v];
 #pragma unroll
         for (uint32_t k = 0; k < 6; ++k) {
-            const uint32_t u = slot_src(g, v, k);
-            const uint32_t i = (k == 0 || k == 5) ? u : u;
-            p.d[k] = load_sel(a.dir_prev, (p.m & slot_bit(k)) != 0u, i, v);
+            p.d[k] = load_sel(a.dir_prev, (p.m & slot_bit(k)) != 0u, slot_src(g, v, k), v);
         }
         if constexpr (PRE) {
 #pragma unroll
@@ -963,6 +961,13 @@ __global__ __launch_bounds__(kBlock) void k_ps_tile(RoundArgs a, TileArgs t) {
             for (uint32_t q = 0; q < kTileMaxNR; ++q) *part_slot(a.parts, (long long)r + NR + q, lane) = 0u;
     }
     __syncthreads();
+    // The gate is checked once per launch: rounds past the target inside this launch still run and
+    // write their buffers, flags and frozen values.  That is exact only because the target is EVERY
+    // participating actor (push-sum: T = nodes, program.fs:178; a line / 2D grid has no inert actor but
+    // the isolated last one): once all have converged no actor sets conv_now again, so no flag or frozen
+    // value changes, and the host reads the state of the converged round's buffer.  A smaller target
+    // would need the per-round gate on the running count (gp_api.cpp enables tiles for push-sum line /
+    // 2D grids only).
     if (prev_s >= a.target) return;
 #pragma unroll
     for (int q = 0; q < NR; ++q) {
