@@ -40,6 +40,9 @@ constexpr size_t kTinyGridMaxActors = 4096;  // ... for the grid topologies too 
 #define GP_TALLY_THR_DIV 8
 #endif
 constexpr size_t kTallyThrDiv = GP_TALLY_THR_DIV;
+#ifndef GP_SPARSE_RAMP
+#define GP_SPARSE_RAMP 1  // A/B knob: full gossip's ramp on lists (k_gs_sparse), one GPU
+#endif
 
 #include <algorithm>
 #include <chrono>
@@ -253,6 +256,12 @@ struct Handle {
                                 // biased (global bit = actor id) and covers its own actors
     uint32_t* dsum = nullptr;   // its summary (one bit per all-done word), from kDsumMinActors actors
     GsTally tally{};            // full gossip on one GPU: receipt tally by target bucket (cnt null: off)
+    // full gossip on one GPU: the ramp's rounds on lists (k_gs_sparse) for rounds < sp_until, a bound the
+    // host extends at every sync from the holder count until it has enqueued a k_gs_full4 round
+    GsSparse gsp{};
+    int64_t sp_until = 0;
+    bool sp_frozen = false;
+    uint32_t* h_spctr = nullptr;  // pinned: the lists' counters and error word, copied after each batch
     // generic push-sum buckets
     uint32_t* bcnt[2] = {nullptr, nullptr};
     uint32_t* boff[2] = {nullptr, nullptr};
@@ -287,6 +296,7 @@ struct Handle {
         if (stream) (void)hipStreamSynchronize(stream);
         for (void* p : allocs) (void)hipFree(p);
         if (h_trace) (void)hipHostFree(h_trace);
+        if (h_spctr) (void)hipHostFree(h_spctr);
         for (hipEvent_t e : kev) (void)hipEventDestroy(e);
         if (ev_a) (void)hipEventDestroy(ev_a);
         if (ev_b) (void)hipEventDestroy(ev_b);
@@ -572,6 +582,16 @@ void gossip_round_plan(Handle* h, int64_t k);
 int ensure_ckpt(Handle* h);
 int ckpt_copy(Handle* h, bool save);
 
+// The rounds after round s that may run on lists (k_gs_sparse) when `holders` actors hold a chain after
+// F(s): a chain starts only on a first receipt, so the holders after F(j) are at most holders * 2^(j - s),
+// and F(r) fits its lists while the holders after F(r - 1) are <= cap.  Returns the first round that
+// does not (exclusive bound).
+int64_t sp_bound(uint32_t cap, int64_t s, uint64_t holders) {
+    int64_t k = 0;
+    while (holders << (k + 1) <= cap && k < 62) ++k;
+    return holders <= cap ? s + 2 + k : s + 1;
+}
+
 int reset(Handle* h) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     const size_t lo = h->lo, n = h->own();
@@ -619,6 +639,14 @@ int reset(Handle* h) {
                 HIP_TRY(hipMemsetAsync(h->tally.chains, 0, (size_t)kPartRing * kParts * kPartStride * sizeof(uint32_t),
                                        h->stream));
                 HIP_TRY(hipMemsetAsync(h->tally.on, 0, 4 * sizeof(uint32_t), h->stream));
+            }
+            if (h->gsp.hl) {  // the holder list is the leader (program.fs:218); every count zero
+                HIP_TRY(hipMemsetAsync(h->gsp.ctr, 0, 3 * 4 * kSpStride * sizeof(uint32_t), h->stream));
+                HIP_TRY(hipMemsetAsync(h->gsp.err, 0, sizeof(uint32_t), h->stream));
+                const uint32_t L = (uint32_t)h->lay.leader;
+                HIP_TRY(hipMemcpyAsync(h->gsp.hl, &L, sizeof L, hipMemcpyHostToDevice, h->stream));
+                h->sp_until = sp_bound(h->gsp.cap, -1, 1);
+                h->sp_frozen = false;
             }
         } else {
             launch_fill_u8(h->dir[0] + xlo, 0xFF, xn, h->stream);
@@ -686,6 +714,8 @@ int reset(Handle* h) {
 
 // Full gossip on one GPU runs the four-actors-per-lane kernel with the done bitmap.
 bool full_quad(const Handle* h) { return h->gossip && h->full && !h->sharded && h->lo == 0; }
+
+
 
 bool fused_marks(const Handle* h) { return kFuseLinkMarks && !h->gossip && !h->generic && !h->sharded && h->g.has_link; }
 
@@ -781,7 +811,10 @@ void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed, int piece = 0,
     if (h->gossip) {
         if (h->generic) {  // adds into inc_cur, consumed (zeroed) by F(k+1)
             if (x) launch_gs_full4x(a, *x, l);
-            else if (full_quad(h)) {
+            else if (full_quad(h) && h->gsp.hl && k < h->sp_until) {
+                launch_gs_sparse(a, h->tally, h->gsp, l);  // the ramp: lists (no tally can be due)
+            } else if (full_quad(h)) {
+                h->sp_frozen = true;  // lists only before the first k_gs_full4 round
                 launch_gs_full4(a, h->tally, l);
                 // the tally's passes exit at once in a round that does not tally; once the synced count
                 // rules the tally out for every later round (fewer than 1/kTallyLateDiv of the nodes
@@ -965,8 +998,21 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         }
         launch_finalize(h->total, h->parts, h->next_kernel - (h->gossip ? 2 : 1), h->stream, h->d_trace, h->rounds,
                         h->tiles);
+        if (h->gsp.hl && !h->sp_frozen) {  // the lists' counters and error word, into pinned memory
+            HIP_TRY(hipMemcpyAsync(h->h_spctr, h->gsp.ctr, 3 * 4 * kSpStride * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   h->stream));
+            HIP_TRY(hipMemcpyAsync(h->h_spctr + 3 * 4 * kSpStride, h->gsp.err, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   h->stream));
+        }
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipStreamSynchronize(h->stream));
+        if (h->gsp.hl && !h->sp_frozen) {  // every round so far ran on lists: extend the bound
+            const uint32_t* c = h->h_spctr;  // (copied behind the batch, before the sync)
+            if (c[3 * 4 * kSpStride]) return fail(GP_EHIP, "k_gs_sparse: a list overflowed its capacity");
+            const int64_t s = h->next_kernel - 1;
+            const uint64_t holders = (uint64_t)c[(0 * 4 + (s & 3)) * kSpStride] + c[(1 * 4 + (s & 3)) * kSpStride];
+            h->sp_until = std::max(h->sp_until, sp_bound(h->gsp.cap, s, holders));
+        }
         int64_t real = B;
         for (int64_t i = 0; i < B; ++i) {
             if ((int64_t)h->h_trace[i] >= h->lay.nodes) {  // ParentActor: count = AllNodes
@@ -1961,6 +2007,24 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
                 const bool fb = (cfg->flags & GP_FLAG_TALLY_FALLBACKS) != 0;
                 t.esc = fb ? 1u : 0xFFFFu;
                 t.onepass = fb ? 0u : 1u;
+            }
+            // the ramp on lists: capacity a quarter of the tally threshold (no round it runs could be
+            // due a tally: its chains stay below thr / 2), or 1/128 of the actors without the tally
+            if (GP_SPARSE_RAMP && full_quad(h) && !h->tiny && !(cfg->flags & GP_FLAG_ONE_ROUND)) {
+                GsSparse& sp = h->gsp;
+                // (a list round costs ~6 us + 0.2 us per 1000 items: below the full walk's ~85 us at 100M
+                // while the holders stay under ~n / 256, profiles/round6/ramp/)
+                const size_t cap = std::min<size_t>(h->tally.cnt ? h->tally.thr / 4u : n, n / 256u);
+                if (cap >= 64 && cap < (1u << 28)) {
+                    sp.cap = (uint32_t)cap;
+                    const size_t size = 2 * cap + kSpSlack;
+                    if ((rc = h->alloc(&sp.hl, size)) || (rc = h->alloc(&sp.tl[0], size)) ||
+                        (rc = h->alloc(&sp.tl[1], size)) || (rc = h->alloc(&sp.ctr, (size_t)3 * 4 * kSpStride)) ||
+                        (rc = h->alloc(&sp.err, 1)))
+                        return bail(rc);
+                    if (hipHostMalloc((void**)&h->h_spctr, (3 * 4 * kSpStride + 1) * sizeof(uint32_t)) != hipSuccess)
+                        return bail(fail(GP_ENOMEM, "hipHostMalloc failed"));
+                }
             }
         } else if ((rc = h->alloc(&h->dir[0], xn, xlo)) || (rc = h->alloc(&h->dir[1], xn, xlo))) {
             return bail(rc);

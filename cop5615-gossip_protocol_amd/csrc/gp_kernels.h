@@ -308,6 +308,22 @@ struct GsTally {
                        // counted batches (the test hook: 0, counted batches everywhere)
 };
 void launch_gs_full4(const RoundArgs& a, const GsTally& t, const Launch& l);  // full gossip, one GPU (lo == 0)
+// Full gossip's ramp on one GPU: while few actors hold a chain, F(r) walks lists instead
+// of every actor — the receipt targets of round r - 1 (apply; a first receipt starts a chain) and the
+// chain holders (emit).  A receipt whose word was 0 lists its target for F(r + 1); a first receipt
+// appends its actor to the holders.  The host runs these rounds while a bound on the holder count (a
+// chain starts only on a first receipt, so holders at most double per round) keeps every list within
+// cap; later rounds run k_gs_full4.  ctr: u32 words kSpStride apart, [field][round & 3]: holders before
+// the round (0), holders added by it (1), receipt targets it listed (2).
+struct GsSparse {
+    uint32_t* hl;     // chain holders (the leader first), 2 cap + kSpSlack
+    uint32_t* tl[2];  // receipt targets of round r, list r & 1
+    uint32_t* ctr;
+    uint32_t* err;    // a list would have overflowed (the host fails the step)
+    uint32_t cap;     // a round runs here only if its holders and last round's targets are <= cap
+};
+constexpr uint32_t kSpStride = 32, kSpSlack = 1024;
+void launch_gs_sparse(const RoundArgs& a, const GsTally& t, const GsSparse& sp, const Launch& l);
 // full gossip on shards: this rank's done-bitmap words into every peer's chunk (after F(k))
 void launch_shard_done_out(const RoundArgs& a, const Xchg& x, hipStream_t s);
 // the scan, scatter and tally passes of a tallied round (each exits at once otherwise)

@@ -2132,6 +2132,112 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
     }
 }
 
+// Full gossip's ramp (GsSparse, gp_kernels.h): F(r) on lists.  Work items [0, tp) apply the receipts
+// of round r - 1 to the listed targets (program.fs:97-105; the receiver drops receipts to done actors,
+// exactly as k_gs_full4's gs_apply4), [tp, tp + hb) are the chain holders, which emit round r
+// (program.fs:89-95, one draw per chain: "full" holds one chain per actor); a first receipt starts a
+// chain, and its actor emits here too.  No sender-side filter (it only saves atomics).  The same gate,
+// counts, done bitmap and tally bookkeeping as k_gs_full4, so a k_gs_full4 round can follow.
+__device__ __forceinline__ uint32_t* sp_ctr(const GsSparse& sp, uint32_t field, uint32_t r) {
+    return sp.ctr + (field * 4u + (r & 3u)) * kSpStride;
+}
+// Append val to list (a wave's wanting lanes, one atomic per wave); every lane of the wave calls it.
+__device__ __forceinline__ void wave_append(bool want, uint32_t val, uint32_t* list, uint32_t* ctr, uint32_t cap,
+                                            uint32_t* err) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const uint32_t lead = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if ((threadIdx.x & 63u) == lead) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, (int)lead, 64);
+    const uint32_t pos = base + mbcnt64(m);
+    if (want) {
+        if (pos < cap) list[pos] = val;
+        else atomicOr(err, 1u);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_gs_sparse(RoundArgs a, GsTally t, GsSparse sp) {
+    const uint32_t r = a.r;
+    unsigned long long prev = 0;
+    if (r) prev = gate_count(a, (long long)r - 1);
+    // round r + 1's tally decision and the chain ring, as k_gs_full4 makes them
+    const double ch = (t.cnt && r >= 1u) ? (double)tally_chains(t, r - 1u) : 0.0;
+    const bool tally_next = t.cnt && r >= 1u && prev < a.target &&
+                            (ch * (double)(a.target - prev) >= (double)t.thr * (double)a.target ||
+                             (kTallyLateDiv && a.dsum && (unsigned long long)GP_GS_FILTER_DIV * prev >= a.target &&
+                              (unsigned long long)(a.target - prev) * kTallyLateDiv >= a.target && ch >= (double)t.thr));
+    if (t.cnt && blockIdx.x == 0 && threadIdx.x < 64) {
+        *part_slot(t.chains, r + 2u, threadIdx.x) = 0u;
+        if (threadIdx.x == 0) {
+            t.on[(r + 1u) & 3u] = tally_next ? 1u : 0u;
+            t.on[r & 3u] = 0u;  // this round does not tally: F(r + 1) reads its receipts from the 32-bit words
+        }
+    }
+    const uint32_t hb = r ? *sp_ctr(sp, 0, r - 1u) + *sp_ctr(sp, 1, r - 1u) : 1u;  // holders after F(r - 1)
+    const uint32_t tp = r ? *sp_ctr(sp, 2, r - 1u) : 0u;                            // round r - 1's targets
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *sp_ctr(sp, 0, r) = hb;
+        *sp_ctr(sp, 1, r + 1u) = 0u;  // the counters F(r + 1) appends to (F(r - 3)'s, read long ago)
+        *sp_ctr(sp, 2, r + 1u) = 0u;
+    }
+    if (r && prev >= a.target) {
+        if (t.cnt && blockIdx.x == 0 && threadIdx.x == 0) t.on[r & 3u] = 0u;
+        return;
+    }
+    const uint32_t size = 2u * sp.cap + kSpSlack;
+    const uint32_t* tprev = sp.tl[(r + 1u) & 1u];
+    uint32_t* tcur = sp.tl[r & 1u];
+    uint32_t newly = 0, chains = 0;
+    const uint32_t nw = tp + hb;
+    for (uint32_t i0 = blockIdx.x * kBlock; i0 < nw; i0 += gridDim.x * kBlock) {
+        const uint32_t i = i0 + threadIdx.x;
+        bool emit = false, newh = false;
+        uint32_t v = 0;
+        if (i < tp) {  // a listed target: its receipts (>= 1) of round r - 1
+            v = tprev[i];
+            const uint32_t inc = a.inc_prev[v];
+            a.inc_prev[v] = 0u;  // round r + 1 adds into this word
+            const uint32_t st = a.gstate[v];
+            uint32_t tok = st & 3u, done = (st >> 2) & 1u;
+            if (inc && !done) {
+                const uint32_t c0 = a.cnt[v], c1 = c0 + inc;
+                a.cnt[v] = c1;
+                if (c0 == 0) {  // program.fs:99-100: a chain starts, and emits this round
+                    ++tok;
+                    newh = emit = true;
+                }
+                if (c0 <= a.threshold && c1 > a.threshold) {  // program.fs:102-104
+                    done = 1u;
+                    ++newly;
+                    const uint32_t bit = 1u << (v & 31u), old = atomicOr(&a.dbits[v >> 5], bit);
+                    if (a.dsum && (old | bit) == ~0u && old != ~0u) atomicOr(&a.dsum[v >> 10], 1u << ((v >> 5) & 31u));
+                }
+                a.gstate[v] = (uint8_t)(tok | (done << 2));
+            }
+        } else if (i < nw) {  // a chain holder
+            v = sp.hl[i - tp];
+            emit = true;
+        }
+        wave_append(newh, v, sp.hl + hb, sp_ctr(sp, 1, r), size - hb, sp.err);
+        bool first = false;
+        uint32_t u0 = 0;
+        if (emit) {
+            const uint4 px = philox(v, r, kStreamGossip, a.seed);
+            const uint32_t t0 = scale_draw(px.x, a.nodes);
+            u0 = t0 + (t0 >= v ? 1u : 0u);
+            first = atomicAdd(&a.inc_cur[u0], 1u) == 0u;
+            ++chains;
+        }
+        wave_append(first, u0, tcur, sp_ctr(sp, 2, r), size, sp.err);
+    }
+    if (r) block_add(newly, a.parts, (long long)r - 1);
+    if (t.cnt) {
+        __syncthreads();  // block_add's LDS slots are reused
+        block_add(chains, t.chains, r);
+    }
+}
+
 // Full gossip on a shard of several ranks: k_gs_full4's walk over this rank's actors
 // [lo, hi), four consecutive actors per lane (the quads of the first and last lanes may hold other
 // ranks' actors, which are masked out: neither applied nor emitted).  Every receipt first takes the
@@ -2916,6 +3022,10 @@ void launch_ps_push_emit(const RoundArgs& a, const Launch& l) {
 
 void launch_ps_push_fill(const RoundArgs& a, uint32_t* slot_cur, const uint32_t* boff_cur, const Launch& l) {
     hipLaunchKernelGGL(k_ps_push_fill, dim3(l.grid), dim3(kBlock), 0, l.stream, a, slot_cur, boff_cur);
+}
+
+void launch_gs_sparse(const RoundArgs& a, const GsTally& t, const GsSparse& sp, const Launch& l) {
+    hipLaunchKernelGGL(k_gs_sparse, dim3(l.grid), dim3(kBlock), 0, l.stream, a, t, sp);
 }
 
 void launch_gs_full4(const RoundArgs& a, const GsTally& t, const Launch& l) {

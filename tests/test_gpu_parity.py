@@ -121,6 +121,27 @@ def test_full_gossip_1m_vs_oracle():
     check_same(gpu, cpu, "gossip")
 
 
+@pytest.mark.parametrize("n,seed", [(20000, 5), (300000, 6), (1_500_000, 7)])
+def test_full_gossip_ramp_lists_vs_oracle(n, seed):
+    """Full gossip's ramp on lists (k_gs_sparse, one GPU): steps of every length, so the host extends
+    its bound on the holders at syncs inside the ramp, and the switch to k_gs_full4 (with the tally from
+    2^20 actors) lands at different rounds; bit-exact against the oracle after every step."""
+    gpu, cpu = _pair(n, "full", "gossip", seed)
+    for chunk in (1, 1, 2, 3, 5, 8, 13, 21, 1 << 20):
+        gs, cs = gpu.step(chunk), cpu.step(chunk, threads=16)
+        assert (gs.round, gs.completed, gs.converged) == (cs.round, cs.completed, cs.converged)
+        check_same(gpu, cpu, "gossip")
+        if gs.converged:
+            break
+    assert gs.converged
+    gpu.reset()  # a second run: the lists start from the leader again
+    gs = gpu.step()
+    assert (gs.round, gs.completed) == (cs.round, cs.completed)
+    check_same(gpu, cpu, "gossip")
+    gpu.close()
+    cpu.close()
+
+
 def test_invalid_config_errors():
     with pytest.raises(GossipError):
         Simulator(0, "line", "gossip")
