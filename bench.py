@@ -117,7 +117,8 @@ def pmc_traffic(kernels, wl: str):
         if not e:
             return None, None
         total += e["hbm_bytes_per_launch"]
-        spans.append(e.get("rounds", "median of the first 60 rounds"))
+        span = e.get("rounds", "median of the first 60 rounds")
+        spans.append(f"{span}, {e['source']}" if e.get("source") else span)
     return total, "; ".join(sorted(set(spans)))
 
 
