@@ -43,6 +43,9 @@ constexpr size_t kTallyThrDiv = GP_TALLY_THR_DIV;
 #ifndef GP_SPARSE_RAMP
 #define GP_SPARSE_RAMP 1  // A/B knob: full gossip's ramp on lists (k_gs_sparse), one GPU
 #endif
+#ifndef GP_SHARD_RAMP
+#define GP_SHARD_RAMP 1  // A/B knob: the same on shards (k_gs_sparse_x)
+#endif
 
 #include <algorithm>
 #include <chrono>
@@ -205,6 +208,7 @@ struct Handle {
         uint32_t dw_out = 0;
     } gpl;
     int64_t bytes_sent = 0;        // exchange bytes this rank sent since the last reset (replays included)
+    int64_t list_rounds = 0;       // full gossip: rounds run on the ramp's lists since the last reset
     const void* last_recv = nullptr;  // the receive buffer of the last gp_shard_deliver
     Ckpt ck;                       // activity tiers: the restore point (push-sum shards)
     int64_t full_until = 0;        // after a restore: the full plan until this many rounds are final
@@ -256,11 +260,13 @@ struct Handle {
                                 // biased (global bit = actor id) and covers its own actors
     uint32_t* dsum = nullptr;   // its summary (one bit per all-done word), from kDsumMinActors actors
     GsTally tally{};            // full gossip on one GPU: receipt tally by target bucket (cnt null: off)
-    // full gossip on one GPU: the ramp's rounds on lists (k_gs_sparse) for rounds < sp_until, a bound the
-    // host extends at every sync from the holder count until it has enqueued a k_gs_full4 round
+    // full gossip: the ramp's rounds on lists (k_gs_sparse; shards k_gs_sparse_x) for rounds < sp_until, a
+    // bound the host extends at every sync from the holder count (shards: every rank's, from the
+    // exchange headers) until it has enqueued a walk over every actor (k_gs_full4 / k_gs_full4x)
     GsSparse gsp{};
     int64_t sp_until = 0;
     bool sp_frozen = false;
+    bool sp_ran = false;          // a list round ran since the last sync (its error word is read there)
     uint32_t* h_spctr = nullptr;  // pinned: the lists' counters and error word, copied after each batch
     // generic push-sum buckets
     uint32_t* bcnt[2] = {nullptr, nullptr};
@@ -640,13 +646,16 @@ int reset(Handle* h) {
                                        h->stream));
                 HIP_TRY(hipMemsetAsync(h->tally.on, 0, 4 * sizeof(uint32_t), h->stream));
             }
-            if (h->gsp.hl) {  // the holder list is the leader (program.fs:218); every count zero
+            if (h->gsp.hl) {  // the holder list is the leader (program.fs:218; a shard's: if it is its actor);
+                              // every count zero
                 HIP_TRY(hipMemsetAsync(h->gsp.ctr, 0, 3 * 4 * kSpStride * sizeof(uint32_t), h->stream));
                 HIP_TRY(hipMemsetAsync(h->gsp.err, 0, sizeof(uint32_t), h->stream));
                 const uint32_t L = (uint32_t)h->lay.leader;
-                HIP_TRY(hipMemcpyAsync(h->gsp.hl, &L, sizeof L, hipMemcpyHostToDevice, h->stream));
+                h->gsp.h0 = L >= h->lo && L < h->hi ? 1u : 0u;
+                if (h->gsp.h0) HIP_TRY(hipMemcpyAsync(h->gsp.hl, &L, sizeof L, hipMemcpyHostToDevice, h->stream));
                 h->sp_until = sp_bound(h->gsp.cap, -1, 1);
                 h->sp_frozen = false;
+                h->sp_ran = false;
             }
         } else {
             launch_fill_u8(h->dir[0] + xlo, 0xFF, xn, h->stream);
@@ -692,6 +701,7 @@ int reset(Handle* h) {
         h->full_until = 0;
         h->last_recv = nullptr;
         h->bytes_sent = 0;
+        h->list_rounds = 0;
         if (h->kpiece > 1 && !h->full_out.empty()) use_layout(h, want_pieces(h));
         if (!h->full_out.empty()) full_plan(h);
         if (gossip_plans(h) && !h->full_out.empty()) {
@@ -810,8 +820,16 @@ void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed, int piece = 0,
     piece_args(h, piece, a, l);
     if (h->gossip) {
         if (h->generic) {  // adds into inc_cur, consumed (zeroed) by F(k+1)
-            if (x) launch_gs_full4x(a, *x, l);
-            else if (full_quad(h) && h->gsp.hl && k < h->sp_until) {
+            const bool lists = h->gsp.hl && !h->sp_frozen && k < h->sp_until;
+            if (x && lists) {
+                h->sp_ran = true;
+                ++h->list_rounds;
+                launch_gs_sparse_x(a, *x, h->gsp, l);  // the ramp on this rank's lists
+            } else if (x) {
+                h->sp_frozen = true;
+                launch_gs_full4x(a, *x, l);
+            } else if (full_quad(h) && lists) {
+                h->sp_ran = true;
                 launch_gs_sparse(a, h->tally, h->gsp, l);  // the ramp: lists (no tally can be due)
             } else if (full_quad(h)) {
                 h->sp_frozen = true;  // lists only before the first k_gs_full4 round
@@ -998,7 +1016,8 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         }
         launch_finalize(h->total, h->parts, h->next_kernel - (h->gossip ? 2 : 1), h->stream, h->d_trace, h->rounds,
                         h->tiles);
-        if (h->gsp.hl && !h->sp_frozen) {  // the lists' counters and error word, into pinned memory
+        const bool sp_read = h->gsp.hl && h->sp_ran;
+        if (sp_read) {  // the lists' counters and error word, into pinned memory
             HIP_TRY(hipMemcpyAsync(h->h_spctr, h->gsp.ctr, 3 * 4 * kSpStride * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                    h->stream));
             HIP_TRY(hipMemcpyAsync(h->h_spctr + 3 * 4 * kSpStride, h->gsp.err, sizeof(uint32_t), hipMemcpyDeviceToHost,
@@ -1006,9 +1025,10 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
         }
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipStreamSynchronize(h->stream));
-        if (h->gsp.hl && !h->sp_frozen) {  // every round so far ran on lists: extend the bound
+        if (sp_read && h->h_spctr[3 * 4 * kSpStride]) return fail(GP_EHIP, "k_gs_sparse: a list overflowed its capacity");
+        h->sp_ran = false;
+        if (sp_read && !h->sp_frozen) {  // every round so far ran on lists: extend the bound
             const uint32_t* c = h->h_spctr;  // (copied behind the batch, before the sync)
-            if (c[3 * 4 * kSpStride]) return fail(GP_EHIP, "k_gs_sparse: a list overflowed its capacity");
             const int64_t s = h->next_kernel - 1;
             const uint64_t holders = (uint64_t)c[(0 * 4 + (s & 3)) * kSpStride] + c[(1 * 4 + (s & 3)) * kSpStride];
             h->sp_until = std::max(h->sp_until, sp_bound(h->gsp.cap, s, holders));
@@ -1436,9 +1456,16 @@ int shard_deliver(Handle* h, const void* recv) {
         const bool face = i == 0 || i == h->npiece - 1;
         const uint32_t per_face = (h->halo + (uint32_t)h->world - 1u) / (uint32_t)h->world;
         uint32_t most = std::max(kSub * h->max_in_cap[i], face ? per_face : 0u);
-        if (h->gossip && h->full)
-            for (int q = 0; q < h->world; ++q) most = std::max(most, (uint32_t)((h->abnd[q + 1] - h->abnd[q]) / 32 + 2));
-        launch_shard_unpack(h->args((uint32_t)k), x, applied_round(h, k), most, h->gossip ? 1 : 0, h->full ? 1 : 0,
+        if (h->gossip && h->full)  // a peer's done part: its pairs' capacity, or every word of its range
+            for (int q = 0; q < h->world; ++q) {
+                const Chunk& c = h->in_chunk[(size_t)i * h->world + q];
+                if (q == h->rank || !c.done) continue;
+                most = std::max(most, c.dpairs ? c.dpairs : (uint32_t)((h->abnd[q + 1] - h->abnd[q]) / 32 + 2));
+            }
+        // F(k) ran on lists (no walk over every actor enqueued yet): the peers' first receipts list
+        // their targets for F(k + 1)
+        const GsSparse sp = h->gsp.hl && !h->sp_frozen ? h->gsp : GsSparse{};
+        launch_shard_unpack(h->args((uint32_t)k), x, applied_round(h, k), most, h->gossip ? 1 : 0, h->full ? 1 : 0, sp,
                             h->stream);
     }
     HIP_TRY(hipGetLastError());
@@ -1655,6 +1682,8 @@ int restore(Handle* h, int64_t reached) {
         h->gpl.seen = false;
         h->gpl.on = false;
     }
+    // the restore point holds the arrays, not the ramp's lists: the replay walks every actor
+    h->sp_frozen = true;
     h->rounds = c.rounds;
     h->completed = c.completed;
     h->converged = false;
@@ -1753,6 +1782,9 @@ int gossip_sync(Handle* h) {
         std::memcpy(&c, ps + kPsChains, sizeof c);
         P.j = h->next_kernel - 1;  // the chains F(next_kernel - 1) emitted
         P.cj = (double)c;
+        // the ramp on lists: every rank's chain holders after F(j) bound this rank's lists (one chain per
+        // holder on "full"), so every rank extends its bound alike
+        if (h->gsp.hl && !h->sp_frozen) h->sp_until = std::max(h->sp_until, sp_bound(h->gsp.cap, P.j, c));
         P.dw_out = ps[kPsDirty];
         for (int q = 0; q < h->world; ++q) {
             P.m_out[q] = ps[kPsOut + q];
@@ -1778,6 +1810,12 @@ int shard_sync(Handle* h, gp_status* st) {
     uint32_t of = 0;
     HIP_TRY(hipMemcpy(&of, h->overflow, sizeof of, hipMemcpyDeviceToHost));
     if (of & 2u) return fail(GP_EOVERFLOW, "a shard received an entry outside its range; the run is void");
+    if (h->gsp.hl && h->sp_ran) {  // (a list cannot outgrow its bound: the counts are exact)
+        uint32_t e = 0;
+        HIP_TRY(hipMemcpy(&e, h->gsp.err, sizeof e, hipMemcpyDeviceToHost));
+        if (e) return fail(GP_EHIP, "k_gs_sparse_x: a list overflowed its capacity");
+        h->sp_ran = false;
+    }
     const int64_t applied = (int64_t)applied_round(h, h->next_kernel - 1) + 1;  // rounds whose counts exist
     int rc;
     if (of) {
@@ -2009,12 +2047,15 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
                 t.onepass = fb ? 0u : 1u;
             }
             // the ramp on lists: capacity a quarter of the tally threshold (no round it runs could be
-            // due a tally: its chains stay below thr / 2), or 1/128 of the actors without the tally
-            if (GP_SPARSE_RAMP && full_quad(h) && !h->tiny && !(cfg->flags & GP_FLAG_ONE_ROUND)) {
+            // due a tally: its chains stay below thr / 2), or 1/256 of the actors without the tally
+            // (shards: a bound on every rank's holders, 1/256 of all the actors and at least 64, so that
+            // every shard run starts on lists; the lists hold this rank's share)
+            if (GP_SPARSE_RAMP && (full_quad(h) || (GP_SHARD_RAMP && gossip_plans(h))) && !h->tiny && !(cfg->flags & GP_FLAG_ONE_ROUND)) {
                 GsSparse& sp = h->gsp;
                 // (a list round costs ~6 us + 0.2 us per 1000 items: below the full walk's ~85 us at 100M
                 // while the holders stay under ~n / 256, profiles/round6/ramp/)
-                const size_t cap = std::min<size_t>(h->tally.cnt ? h->tally.thr / 4u : n, n / 256u);
+                const size_t cap = h->sharded ? std::max<size_t>(A / 256u, 64u)
+                                              : std::min<size_t>(h->tally.cnt ? h->tally.thr / 4u : n, n / 256u);
                 if (cap >= 64 && cap < (1u << 28)) {
                     sp.cap = (uint32_t)cap;
                     const size_t size = 2 * cap + kSpSlack;
@@ -2777,6 +2818,7 @@ int gp_shard_stats(void* handle, gp_shard_counters* out) {
     out->recv_bytes = h->in_poff[h->npiece];
     out->restore_round = h->ck.valid ? h->ck.rounds : -1;
     out->bytes_sent = h->bytes_sent;
+    out->list_rounds = h->list_rounds;
     return GP_OK;
 }
 

@@ -315,15 +315,20 @@ void launch_gs_full4(const RoundArgs& a, const GsTally& t, const Launch& l);  //
 // chain starts only on a first receipt, so holders at most double per round) keeps every list within
 // cap; later rounds run k_gs_full4.  ctr: u32 words kSpStride apart, [field][round & 3]: holders before
 // the round (0), holders added by it (1), receipt targets it listed (2).
+// On shards (k_gs_sparse_x) the lists hold this rank's actors; the bound is on every rank's holders
+// (the global chain count of the exchange headers), and a remote peer's receipts are listed by the
+// unpack (k_shard_unpack, a first receipt of this rank's actor).
 struct GsSparse {
     uint32_t* hl;     // chain holders (the leader first), 2 cap + kSpSlack
     uint32_t* tl[2];  // receipt targets of round r, list r & 1
     uint32_t* ctr;
     uint32_t* err;    // a list would have overflowed (the host fails the step)
     uint32_t cap;     // a round runs here only if its holders and last round's targets are <= cap
+    uint32_t h0;      // holders before round 0: 1 (the leader), on a shard 0 where another rank holds it
 };
 constexpr uint32_t kSpStride = 32, kSpSlack = 1024;
 void launch_gs_sparse(const RoundArgs& a, const GsTally& t, const GsSparse& sp, const Launch& l);
+void launch_gs_sparse_x(const RoundArgs& a, const Xchg& x, const GsSparse& sp, const Launch& l);  // shards
 // full gossip on shards: this rank's done-bitmap words into every peer's chunk (after F(k))
 void launch_shard_done_out(const RoundArgs& a, const Xchg& x, hipStream_t s);
 // the scan, scatter and tally passes of a tallied round (each exits at once otherwise)
@@ -338,9 +343,10 @@ void launch_shard_halo(const RoundArgs& a, const Xchg& x, int pushsum, hipStream
 // headers of round `applied` (-1: none) into every send chunk; zero the per-peer counters
 void launch_shard_pack(const RoundArgs& a, const Xchg& x, long long applied, hipStream_t s);
 // total[applied] from the headers; halo faces into the halo rows of dir_cur / msg_cur; link
-// entries into msg_cur + lcnt_cur / lcnt_cur / inc_cur
+// entries into msg_cur + lcnt_cur / lcnt_cur / inc_cur (full gossip with sp.hl: a first receipt also
+// lists its target in sp.tl[r & 1], the round ran on lists)
 void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, uint32_t max_cap, int gossip,
-                         int full, hipStream_t s);
+                         int full, const GsSparse& sp, hipStream_t s);
 // per-(source piece, destination rank, degree) counts of extra links, for the exchange plan: sb[0..ns]
 // the source pieces' actor bounds (every rank's pieces in order), db[0..nd] the ranks'
 struct HistBounds {

@@ -1163,6 +1163,26 @@ __global__ __launch_bounds__(kBlock) void k_link_count(RoundArgs a) {
         if (nl[j]) a.lcnt_cur[lp[j]] = (uint8_t)(a.ps_tags ? a.tag_cur : nl[j]);
 }
 
+// ------------------------------------------------------------------ full gossip's lists (GsSparse)
+__device__ __forceinline__ uint32_t* sp_ctr(const GsSparse& sp, uint32_t field, uint32_t r) {
+    return sp.ctr + (field * 4u + (r & 3u)) * kSpStride;
+}
+// Append val to list (a wave's wanting lanes, one atomic per wave); every active lane of the wave calls it.
+__device__ __forceinline__ void wave_append(bool want, uint32_t val, uint32_t* list, uint32_t* ctr, uint32_t cap,
+                                            uint32_t* err) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const uint32_t lead = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if ((threadIdx.x & 63u) == lead) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, (int)lead, 64);
+    const uint32_t pos = base + mbcnt64(m);
+    if (want) {
+        if (pos < cap) list[pos] = val;
+        else atomicOr(err, 1u);
+    }
+}
+
 // ------------------------------------------------------------------ shard exchange
 
 
@@ -1430,7 +1450,7 @@ struct SubWalk {
 };
 
 __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, long long applied, int gossip,
-                                                          int full) {
+                                                          int full, GsSparse sp) {
     if (blockIdx.x == 0 && threadIdx.x == 0 && applied >= 0) {
         unsigned long long t = *x.self_newly;
         uint32_t of = 0;
@@ -1543,7 +1563,13 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
             }
             if (full) {  // a receipt for a done actor is dropped (program.fs:92; exact: the state after
                          // F(applied), which F(applied + 1) filters with)
-                if (!(a.dbits && ((a.dbits[t >> 5] >> (t & 31u)) & 1u))) atomicAdd(&a.inc_cur[t], 1u);
+                const bool keep = !(a.dbits && ((a.dbits[t >> 5] >> (t & 31u)) & 1u));
+                if (!sp.hl) {
+                    if (keep) atomicAdd(&a.inc_cur[t], 1u);
+                } else {  // the round ran on lists: a first receipt lists its target for F(r + 1)
+                    const bool first = keep && atomicAdd(&a.inc_cur[t], 1u) == 0u;
+                    wave_append(first, t, sp.tl[a.r & 1u], sp_ctr(sp, 2, a.r), 2u * sp.cap + kSpSlack, sp.err);
+                }
             }
             else if (gossip) a.lcnt_cur[t] = (uint8_t)((e >> 31) + 1u);
             else {  // the slot points at the message where it arrived: one 4-byte store per entry (the
@@ -2138,23 +2164,46 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
 // (program.fs:89-95, one draw per chain: "full" holds one chain per actor); a first receipt starts a
 // chain, and its actor emits here too.  No sender-side filter (it only saves atomics).  The same gate,
 // counts, done bitmap and tally bookkeeping as k_gs_full4, so a k_gs_full4 round can follow.
-__device__ __forceinline__ uint32_t* sp_ctr(const GsSparse& sp, uint32_t field, uint32_t r) {
-    return sp.ctr + (field * 4u + (r & 3u)) * kSpStride;
-}
-// Append val to list (a wave's wanting lanes, one atomic per wave); every lane of the wave calls it.
-__device__ __forceinline__ void wave_append(bool want, uint32_t val, uint32_t* list, uint32_t* ctr, uint32_t cap,
-                                            uint32_t* err) {
-    const uint64_t m = __ballot(want);
-    if (!m) return;
-    const uint32_t lead = (uint32_t)__builtin_ctzll(m);
-    uint32_t base = 0;
-    if ((threadIdx.x & 63u) == lead) base = atomicAdd(ctr, (uint32_t)__popcll(m));
-    base = (uint32_t)__shfl((int)base, (int)lead, 64);
-    const uint32_t pos = base + mbcnt64(m);
-    if (want) {
-        if (pos < cap) list[pos] = val;
-        else atomicOr(err, 1u);
+// F(r)'s list lengths: hb holders after F(r - 1), tp targets of round r - 1 (clamped to the lists: a
+// count past them has set err, and the host fails the step); block 0 records hb and restarts the
+// counters F(r + 1) appends to (F(r - 3)'s, read long ago).
+__device__ __forceinline__ void sp_counts(const GsSparse& sp, uint32_t r, uint32_t& hb, uint32_t& tp) {
+    const uint32_t size = 2u * sp.cap + kSpSlack;
+    hb = r ? *sp_ctr(sp, 0, r - 1u) + *sp_ctr(sp, 1, r - 1u) : sp.h0;
+    tp = r ? *sp_ctr(sp, 2, r - 1u) : 0u;
+    hb = hb < size ? hb : size;
+    tp = tp < size ? tp : size;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *sp_ctr(sp, 0, r) = hb;
+        *sp_ctr(sp, 1, r + 1u) = 0u;
+        *sp_ctr(sp, 2, r + 1u) = 0u;
     }
+}
+// F(r)'s apply of a listed target v (its receipts of round r - 1, >= 1 unless they were all dropped):
+// program.fs:97-105 as k_gs_full4's gs_apply4, the report into the done bitmap.  Returns whether a chain
+// starts (the actor joins the holders and emits this round).
+__device__ __forceinline__ bool sp_apply(const RoundArgs& a, uint32_t v, uint32_t& newly) {
+    const uint32_t inc = a.inc_prev[v];
+    a.inc_prev[v] = 0u;  // round r + 1 adds into this word
+    const uint32_t st = a.gstate[v];
+    uint32_t tok = st & 3u, done = (st >> 2) & 1u;
+    bool start = false;
+    if (inc && !done) {
+        const uint32_t c0 = a.cnt[v], c1 = c0 + inc;
+        a.cnt[v] = c1;
+        if (c0 == 0) {  // program.fs:99-100: a chain starts, and emits this round
+            ++tok;
+            start = true;
+        }
+        if (c0 <= a.threshold && c1 > a.threshold) {  // program.fs:102-104
+            done = 1u;
+            ++newly;
+            const uint32_t bit = 1u << (v & 31u), old = atomicOr(&a.dbits[v >> 5], bit);
+            if (a.dsum && (old | bit) == ~0u && old != ~0u) atomicOr(&a.dsum[v >> 10], 1u << ((v >> 5) & 31u));
+        }
+        a.gstate[v] = (uint8_t)(tok | (done << 2));
+    }
+    return start;
 }
 
 __global__ __launch_bounds__(kBlock) void k_gs_sparse(RoundArgs a, GsTally t, GsSparse sp) {
@@ -2174,13 +2223,8 @@ __global__ __launch_bounds__(kBlock) void k_gs_sparse(RoundArgs a, GsTally t, Gs
             t.on[r & 3u] = 0u;  // this round does not tally: F(r + 1) reads its receipts from the 32-bit words
         }
     }
-    const uint32_t hb = r ? *sp_ctr(sp, 0, r - 1u) + *sp_ctr(sp, 1, r - 1u) : 1u;  // holders after F(r - 1)
-    const uint32_t tp = r ? *sp_ctr(sp, 2, r - 1u) : 0u;                            // round r - 1's targets
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        *sp_ctr(sp, 0, r) = hb;
-        *sp_ctr(sp, 1, r + 1u) = 0u;  // the counters F(r + 1) appends to (F(r - 3)'s, read long ago)
-        *sp_ctr(sp, 2, r + 1u) = 0u;
-    }
+    uint32_t hb, tp;
+    sp_counts(sp, r, hb, tp);
     if (r && prev >= a.target) {
         if (t.cnt && blockIdx.x == 0 && threadIdx.x == 0) t.on[r & 3u] = 0u;
         return;
@@ -2196,25 +2240,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_sparse(RoundArgs a, GsTally t, Gs
         uint32_t v = 0;
         if (i < tp) {  // a listed target: its receipts (>= 1) of round r - 1
             v = tprev[i];
-            const uint32_t inc = a.inc_prev[v];
-            a.inc_prev[v] = 0u;  // round r + 1 adds into this word
-            const uint32_t st = a.gstate[v];
-            uint32_t tok = st & 3u, done = (st >> 2) & 1u;
-            if (inc && !done) {
-                const uint32_t c0 = a.cnt[v], c1 = c0 + inc;
-                a.cnt[v] = c1;
-                if (c0 == 0) {  // program.fs:99-100: a chain starts, and emits this round
-                    ++tok;
-                    newh = emit = true;
-                }
-                if (c0 <= a.threshold && c1 > a.threshold) {  // program.fs:102-104
-                    done = 1u;
-                    ++newly;
-                    const uint32_t bit = 1u << (v & 31u), old = atomicOr(&a.dbits[v >> 5], bit);
-                    if (a.dsum && (old | bit) == ~0u && old != ~0u) atomicOr(&a.dsum[v >> 10], 1u << ((v >> 5) & 31u));
-                }
-                a.gstate[v] = (uint8_t)(tok | (done << 2));
-            }
+            newh = emit = sp_apply(a, v, newly);
         } else if (i < nw) {  // a chain holder
             v = sp.hl[i - tp];
             emit = true;
@@ -2342,6 +2368,82 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
     }
     if (r) block_add(newly, a.parts, (long long)r - 1);
     if (a.cparts) {  // the chains of round r: they size the next rounds' exchange (gp_api.cpp gs_cap)
+        __syncthreads();  // block_add's LDS slots are reused
+        block_add(chains, a.cparts, r);
+    }
+}
+
+// Positions of one entry per thread in peer q's chunk, sub-segment sb (both per thread): LDS counters
+// per (peer, sub-segment), then one global atomic per pair present.  Every thread of the block must
+// call it.
+static_assert(kMaxWorld * kSub == kBlock, "block_reserve_qs: one LDS counter per thread");
+__device__ __forceinline__ uint32_t block_reserve_qs(const Xchg& x, bool want, uint32_t q, uint32_t sb) {
+    __shared__ uint32_t cnt[kMaxWorld * kSub], base[kMaxWorld * kSub];
+    cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t key = q * kSub + sb;
+    const uint32_t pos = want ? atomicAdd(&cnt[key], 1u) : 0u;
+    __syncthreads();
+    if (const uint32_t c = cnt[threadIdx.x]) base[threadIdx.x] = atomicAdd(ctr_at(x, threadIdx.x / kSub, threadIdx.x % kSub), c);
+    __syncthreads();
+    return want ? pos + base[key] : 0u;
+}
+
+// Full gossip's ramp on a shard (GsSparse): k_gs_sparse over this rank's lists — the targets of round
+// r - 1 among its actors (its own receipts and the peers', listed by k_shard_unpack) and its chain
+// holders.  A receipt for one of its actors is a returning atomic (the first lists the target), one
+// for another rank's actor an entry of that rank's chunk, in the sub-segment of the sender's
+// 1024-actor chunk as k_gs_full4x places it (gp_api.cpp sizes the chunks by that rule).  The same
+// counts, chain ring and done bitmap as k_gs_full4x, so a k_gs_full4x round can follow, and each rank
+// may leave its lists in a different round.
+__global__ __launch_bounds__(kBlock) void k_gs_sparse_x(RoundArgs a, Xchg x, GsSparse sp) {
+    const uint32_t r = a.r;
+    if (a.cparts && blockIdx.x == 0 && threadIdx.x < 64) *part_slot(a.cparts, r + 2u, threadIdx.x) = 0u;
+    unsigned long long prev = 0;
+    if (r) prev = gate_count(a, (long long)r - 1);
+    uint32_t hb, tp;
+    sp_counts(sp, r, hb, tp);
+    if (r && prev >= a.target) return;
+    const uint32_t size = 2u * sp.cap + kSpSlack, lo = a.lo, hi = a.hi;
+    const uint32_t* tprev = sp.tl[(r + 1u) & 1u];
+    uint32_t* tcur = sp.tl[r & 1u];
+    uint32_t newly = 0, chains = 0;
+    const uint32_t nw = tp + hb;
+    // block-uniform trip count: block_reserve_qs synchronises the block
+    for (uint32_t i0 = blockIdx.x * kBlock; i0 < nw; i0 += gridDim.x * kBlock) {
+        const uint32_t i = i0 + threadIdx.x;
+        bool emit = false, newh = false;
+        uint32_t v = 0;
+        if (i < tp) {  // a listed target
+            v = tprev[i];
+            newh = emit = sp_apply(a, v, newly);
+        } else if (i < nw) {  // a chain holder
+            v = sp.hl[i - tp];
+            emit = true;
+        }
+        wave_append(newh, v, sp.hl + hb, sp_ctr(sp, 1, r), size - hb, sp.err);
+        bool first = false, remote = false;
+        uint32_t u0 = 0, q = 0;
+        if (emit) {  // program.fs:89-95
+            const uint4 px = philox(v, r, kStreamGossip, a.seed);
+            const uint32_t t0 = scale_draw(px.x, a.nodes);
+            u0 = t0 + (t0 >= v ? 1u : 0u);
+            ++chains;
+            if (u0 - lo < hi - lo) first = atomicAdd(&a.inc_cur[u0], 1u) == 0u;
+            else {
+                remote = true;
+                q = owner(x.abnd, x.world, u0);
+            }
+        }
+        wave_append(first, u0, tcur, sp_ctr(sp, 2, r), size, sp.err);
+        if (__syncthreads_or(remote)) {  // block-uniform
+            const uint32_t sb = (v >> 10) % kSub;
+            const uint32_t pos = block_reserve_qs(x, remote, q, sb);
+            if (remote) put<false>(x, q, pos, u0, make_double2(0.0, 0.0), sb);
+        }
+    }
+    if (r) block_add(newly, a.parts, (long long)r - 1);
+    if (a.cparts) {
         __syncthreads();  // block_add's LDS slots are reused
         block_add(chains, a.cparts, r);
     }
@@ -3099,6 +3201,10 @@ void launch_gs_full4x(const RoundArgs& a, const Xchg& x, const Launch& l) {
     hipLaunchKernelGGL(k_gs_full4x, dim3(l.grid), dim3(kBlock), 0, l.stream, a, x);
 }
 
+void launch_gs_sparse_x(const RoundArgs& a, const Xchg& x, const GsSparse& sp, const Launch& l) {
+    hipLaunchKernelGGL(k_gs_sparse_x, dim3(l.grid), dim3(kBlock), 0, l.stream, a, x, sp);
+}
+
 void launch_shard_halo(const RoundArgs& a, const Xchg& x, int pushsum, hipStream_t s) {
     const uint32_t n = x.h.out_n[0] > x.h.out_n[1] ? x.h.out_n[0] : x.h.out_n[1];
     if (!n) return;
@@ -3112,11 +3218,11 @@ void launch_shard_pack(const RoundArgs& a, const Xchg& x, long long applied, hip
 }
 
 void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, uint32_t max_entries, int gossip,
-                         int full, hipStream_t s) {
+                         int full, const GsSparse& sp, hipStream_t s) {
     const uint32_t cap = (uint32_t)kMaxGrid / x.world;
     uint32_t bpp = (max_entries + kBlock - 1) / kBlock;
     bpp = bpp < 1u ? 1u : (bpp > cap ? cap : bpp);
-    hipLaunchKernelGGL(k_shard_unpack, dim3(bpp * x.world), dim3(kBlock), 0, s, a, x, applied, gossip, full);
+    hipLaunchKernelGGL(k_shard_unpack, dim3(bpp * x.world), dim3(kBlock), 0, s, a, x, applied, gossip, full, sp);
 }
 
 void launch_link_hist(uint64_t seed, const Geom& g, const HistBounds& b, unsigned long long* hist, const Launch& l) {

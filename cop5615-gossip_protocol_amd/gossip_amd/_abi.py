@@ -13,7 +13,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, os.environ.get("GP_LIB", "lib"), "libgossip_hip.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "gossip_hip.h")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 TOPOLOGIES = {"line": 0, "full": 1, "2D": 2, "Imp3D": 3, "3D": 4}
 ALGOS = {"gossip": 0, "push-sum": 1}
 FLAG_KERNEL_TIMING = 1
@@ -64,7 +64,8 @@ class ShardLayout(C.Structure):
 
 class ShardStats(C.Structure):
     _fields_ = [("plan_changes", C.c_int64), ("restores", C.c_int64), ("send_bytes", C.c_int64),
-                ("recv_bytes", C.c_int64), ("restore_round", C.c_int64), ("bytes_sent", C.c_int64)]
+                ("recv_bytes", C.c_int64), ("restore_round", C.c_int64), ("bytes_sent", C.c_int64),
+                ("list_rounds", C.c_int64)]
 
 
 EXPORTS = ["gp_abi_version", "gp_sizes", "gp_create", "gp_reset", "gp_step", "gp_read_gossip",

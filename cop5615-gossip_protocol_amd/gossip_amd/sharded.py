@@ -136,7 +136,8 @@ class HipShard:
         s = _abi.ShardStats()
         _abi.check(self.lib.gp_shard_stats(self.h, C.byref(s)))
         return {"plan_changes": s.plan_changes, "restores": s.restores, "send_bytes": s.send_bytes,
-                "recv_bytes": s.recv_bytes, "restore_round": s.restore_round, "bytes_sent": s.bytes_sent}
+                "recv_bytes": s.recv_bytes, "restore_round": s.restore_round, "bytes_sent": s.bytes_sent,
+                "list_rounds": s.list_rounds}
 
     @property
     def nodes(self) -> int:

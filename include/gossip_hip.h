@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 7
+#define GP_ABI_VERSION 8
 
 /* program.fs:151 "line", :191 "full", :227 "2D", :267 "Imp3D"; "3D" is build-defined (Q9) */
 enum gp_topology { GP_LINE = 0, GP_FULL = 1, GP_TWO_D = 2, GP_IMP3D = 3, GP_THREE_D = 4 };
@@ -243,6 +243,8 @@ typedef struct gp_shard_counters {
     int64_t restore_round;  /* round of the current restore point (-1: none)                     */
     int64_t bytes_sent;     /* exchange bytes this rank sent since the last reset, summed over the
                                rounds packed (replayed rounds included) (ABI 6)                  */
+    int64_t list_rounds;    /* full gossip: rounds this rank ran on its ramp lists since the last
+                               reset (ABI 8)                                                     */
 } gp_shard_counters;
 /* Exchange-plan counters of a shard (num_gpus > 1 handle: rank 0's). */
 int gp_shard_stats(void* handle, gp_shard_counters* out);

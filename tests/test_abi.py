@@ -84,20 +84,20 @@ def test_kstats_struct_layout():
     assert names == [f[0] for f in _abi.KStats._fields_] == [
         "launches", "total_ms", "avg_ms", "bytes_per_launch", "kernel", "aux_avg_ms", "aux_kernel", "work_per_launch"]
     assert _abi.KStats.work_per_launch.offset == 168 and C.sizeof(_abi.KStats) == 176
-    assert _abi.ABI_VERSION == 7 and re.search(r"#define GP_ABI_VERSION 7\b", text)
+    assert _abi.ABI_VERSION == 8 and re.search(r"#define GP_ABI_VERSION 8\b", text)
 
 
 def test_shard_counters_struct_layout():
-    """gp_shard_counters (ABI 5: activity tiers of the shard exchange; ABI 6 appended bytes_sent) as
-    the header lays it out."""
+    """gp_shard_counters (ABI 5: activity tiers of the shard exchange; ABI 6 appended bytes_sent, ABI 8
+    list_rounds) as the header lays it out."""
     import ctypes as C
 
     text = open(_abi.HEADER).read()
     body = re.search(r"typedef struct gp_shard_counters \{(.*?)\} gp_shard_counters;", text, re.S).group(1)
     names = re.findall(r"^\s*int64_t\s+(\w+)", body, re.M)
     assert names == [f[0] for f in _abi.ShardStats._fields_] == [
-        "plan_changes", "restores", "send_bytes", "recv_bytes", "restore_round", "bytes_sent"]
-    assert C.sizeof(_abi.ShardStats) == 48
+        "plan_changes", "restores", "send_bytes", "recv_bytes", "restore_round", "bytes_sent", "list_rounds"]
+    assert C.sizeof(_abi.ShardStats) == 56
 
 
 def test_config_struct_layout():

@@ -318,6 +318,36 @@ def test_full_gossip_round_plans(n, world, seed):
         e.close()
 
 
+@pytest.mark.parametrize("n,world,seed", [(1000, 2, 1), (20000, 3, 4), (300000, 8, 6), (1_500_000, 5, 7)])
+def test_full_gossip_shard_ramp_lists_vs_oracle(n, world, seed):
+    """Full gossip's ramp on shards (k_gs_sparse_x): while every rank's chain holders
+    stay within the lists' bound (1/256 of the actors, at least 64), each rank walks its own lists —
+    the targets of the last round, its own receipts and the ones the peers sent (listed by the
+    unpack), and its holders — then every actor.  Stopped at every round of the ramp and the switch,
+    bit-exact against the oracle each time, and again after a reset."""
+    ref = oracle.OracleSim(n, "full", "gossip", seed=seed)
+    engines = _shards(n, "full", "gossip", world, seed)
+    for rep in range(2):
+        if rep:
+            ref = oracle.OracleSim(n, "full", "gossip", seed=seed)
+            for e in engines:
+                e.reset()
+        for chunk in (1, 1, 1, 2, 3, 5, 8, 13, 21, 1 << 20):
+            rs = ref.step(chunk, threads=8)
+            sts = sharded.run_local(engines, max_rounds=int(rs.round) - int(engines[0].status.round))
+            for st in sts:
+                assert (st.round, st.completed, st.converged) == (rs.round, rs.completed, rs.converged)
+            _check_vs(ref, engines, "gossip")
+            if rs.converged:
+                break
+        assert rs.converged
+        lists = [e.shard_stats()["list_rounds"] for e in engines]
+        # the ramp ran on lists on every rank (the same rounds: the bound is global), not the whole run
+        assert len(set(lists)) == 1 and 4 <= lists[0] < int(rs.round), (lists, int(rs.round))
+    for e in engines:
+        e.close()
+
+
 @pytest.mark.parametrize("n,topo,world,seed", [(20000, "Imp3D", 3, 5), (300000, "Imp3D", 8, 11)])
 def test_group_tight_tiers_vs_oracle(n, topo, world, seed):
     """The library's multi-GPU engine (gp_step over num_gpus shards, here on one device) with

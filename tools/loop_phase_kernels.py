@@ -6,6 +6,8 @@ rounds), and each round to a phase by the global completion count before it (the
 
     python3 tools/loop_phase_kernels.py KT_CSV SERIES_JSON ROUND_KERNEL [world] [warmup rounds, default 8] [bucket]
 
+ROUND_KERNEL: one name, or several separated by commas (full gossip's ramp: k_gs_sparse_x,k_gs_full4x).
+
 bucket: also the tail's rounds in buckets of that many (converged share, kernels and round kernel
 per rank-round).
 """
@@ -22,7 +24,8 @@ def name(r):
 
 
 def main():
-    kt, series, rk = sys.argv[1:4]
+    kt, series, rks = sys.argv[1:4]
+    rks = rks.split(",")
     world = int(sys.argv[4]) if len(sys.argv) > 4 else 8
     warm = int(sys.argv[5]) if len(sys.argv) > 5 else 8
     bucket = int(sys.argv[6]) if len(sys.argv) > 6 else 0
@@ -39,7 +42,7 @@ def main():
     per = defaultdict(lambda: defaultdict(float))  # round -> kernel -> us (all ranks)
     for r in rows:
         n = name(r)
-        if n == rk or n.startswith(rk + "<"):  # (k_ps_quiet_x<false> / <true>)
+        if any(n == rk or n.startswith(rk + "<") for rk in rks):  # (k_ps_quiet_x<false> / <true>)
             if seen < acc:
                 rnd = bisect.bisect_right(starts, seen) - 1 - warm
             else:  # launched past the recorded rounds (one piece each)
@@ -50,12 +53,13 @@ def main():
         per[rnd][n] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     nodes = d.get("nodes") or max(trace)
     prev = [0] + trace[:-1]
-    phases = {"dense (<1% converged)": lambda c: c * 100 < nodes,
-              "mid (1-99% converged)": lambda c: nodes <= c * 100 < 99 * nodes,
-              "tail (>=99% converged)": lambda c: c * 100 >= 99 * nodes,
-              "whole run": lambda c: True}
+    phases = {"dense (<1% converged)": lambda r, c: c * 100 < nodes,
+              "mid (1-99% converged)": lambda r, c: nodes <= c * 100 < 99 * nodes,
+              "tail (>=99% converged)": lambda r, c: c * 100 >= 99 * nodes,
+              "rounds 0-18 (full gossip's ramp)": lambda r, c: r <= 18,
+              "whole run": lambda r, c: True}
     for label, test in phases.items():
-        rs = [r for r in per if r < len(prev) and test(prev[r])]
+        rs = [r for r in per if r < len(prev) and test(r, prev[r])]
         if not rs:
             continue
         ks = sorted({k for r in rs for k in per[r]}, key=lambda k: -sum(per[r].get(k, 0.0) for r in rs))
@@ -68,7 +72,8 @@ def main():
         print(f"tail by {bucket} rounds: rounds, not converged before, kernels / round kernel per rank-round (us)")
         for i in range(0, len(tail), bucket):
             rs = tail[i:i + bucket]
-            rkt = statistics.fmean(sum(v for k, v in per[r].items() if k == rk or k.startswith(rk + "<")) for r in rs)
+            rkt = statistics.fmean(sum(v for k, v in per[r].items() if any(k == rk or k.startswith(rk + "<") for rk in rks))
+                                   for r in rs)
             tot = statistics.fmean(sum(per[r].values()) for r in rs)
             print(f"  {rs[0]:5d}..{rs[-1]:<5d} {1 - prev[rs[0]] / nodes:8.5f} {tot / world:8.1f} {rkt / world:8.1f}")
 
