@@ -267,6 +267,9 @@ struct Handle {
     int64_t sp_until = 0;
     bool sp_frozen = false;
     bool sp_ran = false;          // a list round ran since the last sync (its error word is read there)
+    int64_t sp_fused = -1;        // shards: the round whose list kernel also ran its done-word pass and pack
+    int64_t sp_s = -1;            // the last synced holder count: sp_h holders (shards: every rank's)
+    uint64_t sp_h = 1;            // after F(sp_s), which sizes a list round's grid
     uint32_t* h_spctr = nullptr;  // pinned: the lists' counters and error word, copied after each batch
     // generic push-sum buckets
     uint32_t* bcnt[2] = {nullptr, nullptr};
@@ -648,7 +651,7 @@ int reset(Handle* h) {
             }
             if (h->gsp.hl) {  // the holder list is the leader (program.fs:218; a shard's: if it is its actor);
                               // every count zero
-                HIP_TRY(hipMemsetAsync(h->gsp.ctr, 0, 3 * 4 * kSpStride * sizeof(uint32_t), h->stream));
+                HIP_TRY(hipMemsetAsync(h->gsp.ctr, 0, (3 * 4 + 1) * kSpStride * sizeof(uint32_t), h->stream));  // (+ fin)
                 HIP_TRY(hipMemsetAsync(h->gsp.err, 0, sizeof(uint32_t), h->stream));
                 const uint32_t L = (uint32_t)h->lay.leader;
                 h->gsp.h0 = L >= h->lo && L < h->hi ? 1u : 0u;
@@ -656,6 +659,9 @@ int reset(Handle* h) {
                 h->sp_until = sp_bound(h->gsp.cap, -1, 1);
                 h->sp_frozen = false;
                 h->sp_ran = false;
+                h->sp_s = -1;
+                h->sp_h = 1;
+                h->sp_fused = -1;
             }
         } else {
             launch_fill_u8(h->dir[0] + xlo, 0xFF, xn, h->stream);
@@ -804,6 +810,17 @@ void piece_args(const Handle* h, int piece, RoundArgs& a, Launch& l) {
     a.span = span_for(a.hi - a.lo, l.grid);
 }
 
+// A list round's grid: one thread per item at most.  F(k)'s items (the holders after F(k - 1) and the
+// targets of round k - 1, at most as many) are bounded by the synced holder count, doubled per round
+// since (a chain starts only on a first receipt).
+constexpr int kSpFusedGrid = 256;
+Launch sp_launch(const Handle* h, int64_t k, Launch l) {
+    const int64_t d = std::min<int64_t>(std::max<int64_t>(k - 1 - h->sp_s, 0), 40);
+    const double items = 2.0 * (double)h->sp_h * std::ldexp(1.0, (int)d);
+    l.grid = (int)std::max(1.0, std::min((double)l.grid, std::ceil(items / (double)kBlock)));
+    return l;
+}
+
 void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed, int piece = 0, int nr = 1) {
     RoundArgs a = h->args((uint32_t)k);
     if (h->tiles) {
@@ -821,16 +838,19 @@ void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed, int piece = 0,
     if (h->gossip) {
         if (h->generic) {  // adds into inc_cur, consumed (zeroed) by F(k+1)
             const bool lists = h->gsp.hl && !h->sp_frozen && k < h->sp_until;
-            if (x && lists) {
+            if (x && lists) {  // the ramp on this rank's lists; the round's passes in its last block
                 h->sp_ran = true;
+                h->sp_fused = k;
                 ++h->list_rounds;
-                launch_gs_sparse_x(a, *x, h->gsp, l);  // the ramp on this rank's lists
+                Launch ls = sp_launch(h, k, l);
+                ls.grid = std::min(ls.grid, kSpFusedGrid);  // (the last-block count: one atomic per block)
+                launch_gs_sparse_x(a, *x, h->gsp, h->gossip ? (long long)k - 1 : (long long)k, ls);
             } else if (x) {
                 h->sp_frozen = true;
                 launch_gs_full4x(a, *x, l);
             } else if (full_quad(h) && lists) {
                 h->sp_ran = true;
-                launch_gs_sparse(a, h->tally, h->gsp, l);  // the ramp: lists (no tally can be due)
+                launch_gs_sparse(a, h->tally, h->gsp, sp_launch(h, k, l));  // the ramp: lists (no tally can be due)
             } else if (full_quad(h)) {
                 h->sp_frozen = true;  // lists only before the first k_gs_full4 round
                 launch_gs_full4(a, h->tally, l);
@@ -872,7 +892,8 @@ int launch_aux(Handle* h, int64_t k, const Xchg* x, int piece = 0) {
             if (x) launch_gs_link_scatter_x(a, *x, l);
             else launch_link_count(a, l);
         }
-        if (h->generic && x && h->world > 1) launch_shard_done_out(a, *x, h->stream);
+        // (a list round's last block ran it: k_gs_sparse_x)
+        if (h->generic && x && h->world > 1 && h->sp_fused != k) launch_shard_done_out(a, *x, h->stream);
     } else if (h->generic) {
         const int c = (int)(r & 1u);
         launch_exclusive_scan(h->bcnt[c], h->boff[c], h->g.actors, h->scan_scratch, h->stream);
@@ -1032,6 +1053,8 @@ int step(Handle* h, int64_t max_rounds, gp_status* st) {
             const int64_t s = h->next_kernel - 1;
             const uint64_t holders = (uint64_t)c[(0 * 4 + (s & 3)) * kSpStride] + c[(1 * 4 + (s & 3)) * kSpStride];
             h->sp_until = std::max(h->sp_until, sp_bound(h->gsp.cap, s, holders));
+            h->sp_s = s;
+            h->sp_h = holders;
         }
         int64_t real = B;
         for (int64_t i = 0; i < B; ++i) {
@@ -1415,7 +1438,7 @@ int shard_round_piece(Handle* h, void* send, int piece) {
     // the halo face this piece holds (the rank's first actors to rank-1, its last to rank+1), then the
     // headers
     if (!x.hin) launch_shard_halo(a, x, h->gossip ? 0 : 1, h->stream);
-    launch_shard_pack(a, x, applied_round(h, k), h->stream);
+    if (h->sp_fused != k) launch_shard_pack(a, x, applied_round(h, k), h->stream);  // (a list round packed itself)
     HIP_TRY(hipGetLastError());
     for (int q = 0; q < h->world; ++q) h->bytes_sent += (int64_t)h->out_chunk[(size_t)piece * h->world + q].size;
     if (++h->piece_next == h->npiece) {
@@ -1684,6 +1707,7 @@ int restore(Handle* h, int64_t reached) {
     }
     // the restore point holds the arrays, not the ramp's lists: the replay walks every actor
     h->sp_frozen = true;
+    h->sp_fused = -1;
     h->rounds = c.rounds;
     h->completed = c.completed;
     h->converged = false;
@@ -1784,7 +1808,11 @@ int gossip_sync(Handle* h) {
         P.cj = (double)c;
         // the ramp on lists: every rank's chain holders after F(j) bound this rank's lists (one chain per
         // holder on "full"), so every rank extends its bound alike
-        if (h->gsp.hl && !h->sp_frozen) h->sp_until = std::max(h->sp_until, sp_bound(h->gsp.cap, P.j, c));
+        if (h->gsp.hl && !h->sp_frozen) {
+            h->sp_until = std::max(h->sp_until, sp_bound(h->gsp.cap, P.j, c));
+            h->sp_s = P.j;
+            h->sp_h = c;
+        }
         P.dw_out = ps[kPsDirty];
         for (int q = 0; q < h->world; ++q) {
             P.m_out[q] = ps[kPsOut + q];
@@ -2060,9 +2088,10 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
                     sp.cap = (uint32_t)cap;
                     const size_t size = 2 * cap + kSpSlack;
                     if ((rc = h->alloc(&sp.hl, size)) || (rc = h->alloc(&sp.tl[0], size)) ||
-                        (rc = h->alloc(&sp.tl[1], size)) || (rc = h->alloc(&sp.ctr, (size_t)3 * 4 * kSpStride)) ||
+                        (rc = h->alloc(&sp.tl[1], size)) || (rc = h->alloc(&sp.ctr, (size_t)3 * 4 * kSpStride + kSpStride)) ||
                         (rc = h->alloc(&sp.err, 1)))
                         return bail(rc);
+                    sp.fin = sp.ctr + 3 * 4 * kSpStride;  // (its own line, after the counters)
                     if (hipHostMalloc((void**)&h->h_spctr, (3 * 4 * kSpStride + 1) * sizeof(uint32_t)) != hipSuccess)
                         return bail(fail(GP_ENOMEM, "hipHostMalloc failed"));
                 }

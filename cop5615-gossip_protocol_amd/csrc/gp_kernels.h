@@ -310,8 +310,8 @@ struct GsTally {
 void launch_gs_full4(const RoundArgs& a, const GsTally& t, const Launch& l);  // full gossip, one GPU (lo == 0)
 // Full gossip's ramp on one GPU: while few actors hold a chain, F(r) walks lists instead
 // of every actor — the receipt targets of round r - 1 (apply; a first receipt starts a chain) and the
-// chain holders (emit).  A receipt whose word was 0 lists its target for F(r + 1); a first receipt
-// appends its actor to the holders.  The host runs these rounds while a bound on the holder count (a
+// chain holders (emit).  Every receipt lists its target for F(r + 1) (a target listed twice is applied
+// once); a first receipt appends its actor to the holders.  The host runs these rounds while a bound on the holder count (a
 // chain starts only on a first receipt, so holders at most double per round) keeps every list within
 // cap; later rounds run k_gs_full4.  ctr: u32 words kSpStride apart, [field][round & 3]: holders before
 // the round (0), holders added by it (1), receipt targets it listed (2).
@@ -325,10 +325,13 @@ struct GsSparse {
     uint32_t* err;    // a list would have overflowed (the host fails the step)
     uint32_t cap;     // a round runs here only if its holders and last round's targets are <= cap
     uint32_t h0;      // holders before round 0: 1 (the leader), on a shard 0 where another rank holds it
+    uint32_t* fin;    // shards: blocks of k_gs_sparse_x finished (its last block runs the done-word pass
+                      // and the pack; 0 between launches)
 };
 constexpr uint32_t kSpStride = 32, kSpSlack = 1024;
 void launch_gs_sparse(const RoundArgs& a, const GsTally& t, const GsSparse& sp, const Launch& l);
-void launch_gs_sparse_x(const RoundArgs& a, const Xchg& x, const GsSparse& sp, const Launch& l);  // shards
+// shards: F(k) on lists, then (its last block) k_shard_done_out's and k_shard_pack's work for round k
+void launch_gs_sparse_x(const RoundArgs& a, const Xchg& x, const GsSparse& sp, long long applied, const Launch& l);
 // full gossip on shards: this rank's done-bitmap words into every peer's chunk (after F(k))
 void launch_shard_done_out(const RoundArgs& a, const Xchg& x, hipStream_t s);
 // the scan, scatter and tally passes of a tallied round (each exits at once otherwise)
@@ -343,7 +346,7 @@ void launch_shard_halo(const RoundArgs& a, const Xchg& x, int pushsum, hipStream
 // headers of round `applied` (-1: none) into every send chunk; zero the per-peer counters
 void launch_shard_pack(const RoundArgs& a, const Xchg& x, long long applied, hipStream_t s);
 // total[applied] from the headers; halo faces into the halo rows of dir_cur / msg_cur; link
-// entries into msg_cur + lcnt_cur / lcnt_cur / inc_cur (full gossip with sp.hl: a first receipt also
+// entries into msg_cur + lcnt_cur / lcnt_cur / inc_cur (full gossip with sp.hl: every receipt also
 // lists its target in sp.tl[r & 1], the round ran on lists)
 void launch_shard_unpack(const RoundArgs& a, const Xchg& x, long long applied, uint32_t max_cap, int gossip,
                          int full, const GsSparse& sp, hipStream_t s);

@@ -1182,6 +1182,28 @@ __device__ __forceinline__ void wave_append(bool want, uint32_t val, uint32_t* l
         else atomicOr(err, 1u);
     }
 }
+// Two appends at once (the wave's first active lane issues both counters' atomics, then one wait).
+__device__ __forceinline__ void wave_append2(bool w1, uint32_t v1, uint32_t* l1, uint32_t* c1, uint32_t cap1, bool w2,
+                                             uint32_t v2, uint32_t* l2, uint32_t* c2, uint32_t cap2, uint32_t* err) {
+    const uint64_t m1 = __ballot(w1), m2 = __ballot(w2);
+    if (!(m1 | m2)) return;
+    const uint32_t lead = (uint32_t)__builtin_ctzll(__ballot(true));
+    uint32_t b1 = 0, b2 = 0;
+    if ((threadIdx.x & 63u) == lead) {
+        if (m1) b1 = atomicAdd(c1, (uint32_t)__popcll(m1));
+        if (m2) b2 = atomicAdd(c2, (uint32_t)__popcll(m2));
+    }
+    b1 = (uint32_t)__shfl((int)b1, (int)lead, 64) + mbcnt64(m1);
+    b2 = (uint32_t)__shfl((int)b2, (int)lead, 64) + mbcnt64(m2);
+    if (w1) {
+        if (b1 < cap1) l1[b1] = v1;
+        else atomicOr(err, 1u);
+    }
+    if (w2) {
+        if (b2 < cap2) l2[b2] = v2;
+        else atomicOr(err, 1u);
+    }
+}
 
 // ------------------------------------------------------------------ shard exchange
 
@@ -1338,7 +1360,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_halo(RoundArgs a, Xchg x, int 
 // of kMaxWorld x kSub threads: thread (q, s) handles sub-segment s of peer q, all at once.
 static_assert(kMaxWorld * kSub == kBlock, "k_shard_pack maps one thread per (peer, sub-segment)");
 
-__global__ __launch_bounds__(kBlock) void k_shard_pack(RoundArgs a, Xchg x, long long applied) {
+__device__ __forceinline__ void shard_pack_body(const RoundArgs& a, const Xchg& x, long long applied) {
     __shared__ unsigned long long newly_s, chains_s;
     __shared__ uint32_t of_s[kMaxWorld], max_s[kMaxWorld], last_s[kMaxWorld], dirty_s;
     if (threadIdx.x < 64) {
@@ -1415,6 +1437,10 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(RoundArgs a, Xchg x, long
         x.dstat[kDstatLeft] = left ? 1u : 0u;
         x.pstat[kPsDirty] = dirty_s;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_shard_pack(RoundArgs a, Xchg x, long long applied) {
+    shard_pack_body(a, x, applied);
 }
 
 // total[applied] = total[applied-1] + every rank's count; the received link entries land in
@@ -1563,12 +1589,13 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
             }
             if (full) {  // a receipt for a done actor is dropped (program.fs:92; exact: the state after
                          // F(applied), which F(applied + 1) filters with)
-                const bool keep = !(a.dbits && ((a.dbits[t >> 5] >> (t & 31u)) & 1u));
                 if (!sp.hl) {
-                    if (keep) atomicAdd(&a.inc_cur[t], 1u);
-                } else {  // the round ran on lists: a first receipt lists its target for F(r + 1)
-                    const bool first = keep && atomicAdd(&a.inc_cur[t], 1u) == 0u;
-                    wave_append(first, t, sp.tl[a.r & 1u], sp_ctr(sp, 2, a.r), 2u * sp.cap + kSpSlack, sp.err);
+                    if (!(a.dbits && ((a.dbits[t >> 5] >> (t & 31u)) & 1u))) atomicAdd(&a.inc_cur[t], 1u);
+                } else {  // the round ran on lists: every receipt lists its target for F(r + 1), which
+                          // drops the receipts of a done actor itself (k_gs_sparse_x / gs_apply4), as
+                          // the list rounds' local receipts are dropped: no bitmap read on the way
+                    atomicAdd(&a.inc_cur[t], 1u);
+                    wave_append(true, t, sp.tl[a.r & 1u], sp_ctr(sp, 2, a.r), 2u * sp.cap + kSpSlack, sp.err);
                 }
             }
             else if (gossip) a.lcnt_cur[t] = (uint8_t)((e >> 31) + 1u);
@@ -2162,8 +2189,10 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4(RoundArgs a, GsTally t) {
 // of round r - 1 to the listed targets (program.fs:97-105; the receiver drops receipts to done actors,
 // exactly as k_gs_full4's gs_apply4), [tp, tp + hb) are the chain holders, which emit round r
 // (program.fs:89-95, one draw per chain: "full" holds one chain per actor); a first receipt starts a
-// chain, and its actor emits here too.  No sender-side filter (it only saves atomics).  The same gate,
-// counts, done bitmap and tally bookkeeping as k_gs_full4, so a k_gs_full4 round can follow.
+// chain, and its actor emits here too.  Every receipt lists its target (a target listed twice takes
+// its count once: the apply exchanges the word with 0), so no atomic on the way waits for its result
+// but the lists' own.  No sender-side filter (it only saves atomics).  The same gate, counts, done
+// bitmap and tally bookkeeping as k_gs_full4, so a k_gs_full4 round can follow.
 // F(r)'s list lengths: hb holders after F(r - 1), tp targets of round r - 1 (clamped to the lists: a
 // count past them has set err, and the host fails the step); block 0 records hb and restarts the
 // counters F(r + 1) appends to (F(r - 3)'s, read long ago).
@@ -2179,12 +2208,11 @@ __device__ __forceinline__ void sp_counts(const GsSparse& sp, uint32_t r, uint32
         *sp_ctr(sp, 2, r + 1u) = 0u;
     }
 }
-// F(r)'s apply of a listed target v (its receipts of round r - 1, >= 1 unless they were all dropped):
-// program.fs:97-105 as k_gs_full4's gs_apply4, the report into the done bitmap.  Returns whether a chain
-// starts (the actor joins the holders and emits this round).
+// F(r)'s apply of a listed target v (its receipts of round r - 1; 0 where an earlier copy of the entry
+// took them): program.fs:97-105 as k_gs_full4's gs_apply4, the report into the done bitmap.  Returns
+// whether a chain starts (the actor joins the holders and emits this round).
 __device__ __forceinline__ bool sp_apply(const RoundArgs& a, uint32_t v, uint32_t& newly) {
-    const uint32_t inc = a.inc_prev[v];
-    a.inc_prev[v] = 0u;  // round r + 1 adds into this word
+    const uint32_t inc = atomicExch(&a.inc_prev[v], 0u);  // round r + 1 adds into this word
     const uint32_t st = a.gstate[v];
     uint32_t tok = st & 3u, done = (st >> 2) & 1u;
     bool start = false;
@@ -2245,17 +2273,15 @@ __global__ __launch_bounds__(kBlock) void k_gs_sparse(RoundArgs a, GsTally t, Gs
             v = sp.hl[i - tp];
             emit = true;
         }
-        wave_append(newh, v, sp.hl + hb, sp_ctr(sp, 1, r), size - hb, sp.err);
-        bool first = false;
         uint32_t u0 = 0;
         if (emit) {
             const uint4 px = philox(v, r, kStreamGossip, a.seed);
             const uint32_t t0 = scale_draw(px.x, a.nodes);
             u0 = t0 + (t0 >= v ? 1u : 0u);
-            first = atomicAdd(&a.inc_cur[u0], 1u) == 0u;
+            atomicAdd(&a.inc_cur[u0], 1u);
             ++chains;
         }
-        wave_append(first, u0, tcur, sp_ctr(sp, 2, r), size, sp.err);
+        wave_append2(newh, v, sp.hl + hb, sp_ctr(sp, 1, r), size - hb, emit, u0, tcur, sp_ctr(sp, 2, r), size, sp.err);
     }
     if (r) block_add(newly, a.parts, (long long)r - 1);
     if (t.cnt) {
@@ -2389,21 +2415,67 @@ __device__ __forceinline__ uint32_t block_reserve_qs(const Xchg& x, bool want, u
     return want ? pos + base[key] : 0u;
 }
 
+// Full gossip on shards: this rank's words of the done bitmap (after F(r)) into every peer's chunk.
+// The peers' replicas only feed the sender-side filter, which stays exact however stale they are
+// (done only turns on; the receiver filters exactly), so words are shipped lazily: a word goes out
+// when it differs from what was last shipped (x.dship).  The plan's done part is either every word
+// of the range (dpairs 0: the receivers read them all when any changed) or up to dpairs (index,
+// word) pairs; words past that capacity stay dirty for a later round (x.dstat backlog flag).  Every
+// peer gets the same words.
+// (blocks bid of nblk: the pass's grid, or the one block that ends a list round, k_gs_sparse_x)
+__device__ __forceinline__ void done_out_body(const RoundArgs& a, const Xchg& x, uint32_t bid, uint32_t nblk) {
+    if (applied_converged(a)) return;  // block-uniform
+    // none of this rank's actors reported in the round F(r) applied and no word is left over: no word
+    // differs from what was shipped (the early rounds of a run); the header's counts stay 0
+    const uint32_t newly = a.r ? wave_sum(*part_slot(a.parts, (long long)a.r - 1, threadIdx.x & 63u)) : 0u;
+    if (!newly && !x.dstat[kDstatLeft]) return;  // uniform: every wave sums the same final sub-counters
+    uint32_t dp = 0;
+    bool any = false;
+    for (uint32_t q = 0; q < x.world && !any; ++q)
+        if (q != x.rank && x.out[q].done) {
+            dp = x.out[q].dpairs;  // the sender's plan: the same for every peer
+            any = true;
+        }
+    if (!any) return;
+    const uint32_t w0 = a.lo >> 5, nw = ((a.hi - 1u) >> 5) - w0 + 1u;
+    // block-uniform trip count: every thread reaches block_reserve1
+    for (uint32_t base = bid * kBlock; base < nw; base += nblk * kBlock) {
+        const uint32_t i = base + threadIdx.x;
+        const bool valid = i < nw;
+        const uint32_t val = valid ? a.dbits[w0 + i] : 0u;
+        const bool dirty = valid && val != x.dship[w0 + i];
+        const uint32_t pos = block_reserve1(&x.dstat[kDstatCount], dirty);
+        if (!dp) {  // every word
+            if (valid)
+                for (uint32_t q = 0; q < x.world; ++q)
+                    if (q != x.rank && x.out[q].done) x.out[q].done[i] = val;
+            if (dirty) x.dship[w0 + i] = val;
+        } else if (dirty && pos < dp) {
+            for (uint32_t q = 0; q < x.world; ++q)
+                if (q != x.rank && x.out[q].done) reinterpret_cast<uint2*>(x.out[q].done)[pos] = make_uint2(w0 + i, val);
+            x.dship[w0 + i] = val;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_shard_done_out(RoundArgs a, Xchg x) { done_out_body(a, x, blockIdx.x, gridDim.x); }
+
 // Full gossip's ramp on a shard (GsSparse): k_gs_sparse over this rank's lists — the targets of round
 // r - 1 among its actors (its own receipts and the peers', listed by k_shard_unpack) and its chain
-// holders.  A receipt for one of its actors is a returning atomic (the first lists the target), one
-// for another rank's actor an entry of that rank's chunk, in the sub-segment of the sender's
+// holders.  A receipt for one of its actors is an atomic and a list entry, one for another rank's
+// actor an entry of that rank's chunk, in the sub-segment of the sender's
 // 1024-actor chunk as k_gs_full4x places it (gp_api.cpp sizes the chunks by that rule).  The same
 // counts, chain ring and done bitmap as k_gs_full4x, so a k_gs_full4x round can follow, and each rank
-// may leave its lists in a different round.
-__global__ __launch_bounds__(kBlock) void k_gs_sparse_x(RoundArgs a, Xchg x, GsSparse sp) {
+// may leave its lists in a different round.  Its last block also runs the round's two passes after it
+// (k_shard_done_out, k_shard_pack).
+__global__ __launch_bounds__(kBlock) void k_gs_sparse_x(RoundArgs a, Xchg x, GsSparse sp, long long applied) {
     const uint32_t r = a.r;
     if (a.cparts && blockIdx.x == 0 && threadIdx.x < 64) *part_slot(a.cparts, r + 2u, threadIdx.x) = 0u;
     unsigned long long prev = 0;
     if (r) prev = gate_count(a, (long long)r - 1);
     uint32_t hb, tp;
     sp_counts(sp, r, hb, tp);
-    if (r && prev >= a.target) return;
+    if (r && prev >= a.target) hb = tp = 0u;  // converged: no work, the headers still go out
     const uint32_t size = 2u * sp.cap + kSpSlack, lo = a.lo, hi = a.hi;
     const uint32_t* tprev = sp.tl[(r + 1u) & 1u];
     uint32_t* tcur = sp.tl[r & 1u];
@@ -2421,21 +2493,19 @@ __global__ __launch_bounds__(kBlock) void k_gs_sparse_x(RoundArgs a, Xchg x, GsS
             v = sp.hl[i - tp];
             emit = true;
         }
-        wave_append(newh, v, sp.hl + hb, sp_ctr(sp, 1, r), size - hb, sp.err);
-        bool first = false, remote = false;
+        bool local = false, remote = false;
         uint32_t u0 = 0, q = 0;
         if (emit) {  // program.fs:89-95
             const uint4 px = philox(v, r, kStreamGossip, a.seed);
             const uint32_t t0 = scale_draw(px.x, a.nodes);
             u0 = t0 + (t0 >= v ? 1u : 0u);
             ++chains;
-            if (u0 - lo < hi - lo) first = atomicAdd(&a.inc_cur[u0], 1u) == 0u;
-            else {
-                remote = true;
-                q = owner(x.abnd, x.world, u0);
-            }
+            local = u0 - lo < hi - lo;
+            remote = !local;
+            if (local) atomicAdd(&a.inc_cur[u0], 1u);
+            else q = owner(x.abnd, x.world, u0);
         }
-        wave_append(first, u0, tcur, sp_ctr(sp, 2, r), size, sp.err);
+        wave_append2(newh, v, sp.hl + hb, sp_ctr(sp, 1, r), size - hb, local, u0, tcur, sp_ctr(sp, 2, r), size, sp.err);
         if (__syncthreads_or(remote)) {  // block-uniform
             const uint32_t sb = (v >> 10) % kSub;
             const uint32_t pos = block_reserve_qs(x, remote, q, sb);
@@ -2447,48 +2517,22 @@ __global__ __launch_bounds__(kBlock) void k_gs_sparse_x(RoundArgs a, Xchg x, GsS
         __syncthreads();  // block_add's LDS slots are reused
         block_add(chains, a.cparts, r);
     }
-}
-
-// Full gossip on shards: this rank's words of the done bitmap (after F(r)) into every peer's chunk.
-// The peers' replicas only feed the sender-side filter, which stays exact however stale they are
-// (done only turns on; the receiver filters exactly), so words are shipped lazily: a word goes out
-// when it differs from what was last shipped (x.dship).  The plan's done part is either every word
-// of the range (dpairs 0: the receivers read them all when any changed) or up to dpairs (index,
-// word) pairs; words past that capacity stay dirty for a later round (x.dstat backlog flag).  Every
-// peer gets the same words.
-__global__ __launch_bounds__(kBlock) void k_shard_done_out(RoundArgs a, Xchg x) {
-    if (applied_converged(a)) return;  // block-uniform
-    // none of this rank's actors reported in the round F(r) applied and no word is left over: no word
-    // differs from what was shipped (the early rounds of a run); the header's counts stay 0
-    const uint32_t newly = a.r ? wave_sum(*part_slot(a.parts, (long long)a.r - 1, threadIdx.x & 63u)) : 0u;
-    if (!newly && !x.dstat[kDstatLeft]) return;  // uniform: every wave sums the same final sub-counters
-    uint32_t dp = 0;
-    bool any = false;
-    for (uint32_t q = 0; q < x.world && !any; ++q)
-        if (q != x.rank && x.out[q].done) {
-            dp = x.out[q].dpairs;  // the sender's plan: the same for every peer
-            any = true;
-        }
-    if (!any) return;
-    const uint32_t w0 = a.lo >> 5, nw = ((a.hi - 1u) >> 5) - w0 + 1u;
-    // block-uniform trip count: every thread reaches block_reserve1
-    for (uint32_t base = blockIdx.x * kBlock; base < nw; base += gridDim.x * kBlock) {
-        const uint32_t i = base + threadIdx.x;
-        const bool valid = i < nw;
-        const uint32_t val = valid ? a.dbits[w0 + i] : 0u;
-        const bool dirty = valid && val != x.dship[w0 + i];
-        const uint32_t pos = block_reserve1(&x.dstat[kDstatCount], dirty);
-        if (!dp) {  // every word
-            if (valid)
-                for (uint32_t q = 0; q < x.world; ++q)
-                    if (q != x.rank && x.out[q].done) x.out[q].done[i] = val;
-            if (dirty) x.dship[w0 + i] = val;
-        } else if (dirty && pos < dp) {
-            for (uint32_t q = 0; q < x.world; ++q)
-                if (q != x.rank && x.out[q].done) reinterpret_cast<uint2*>(x.out[q].done)[pos] = make_uint2(w0 + i, val);
-            x.dship[w0 + i] = val;
-        }
+    // The block that finishes last ends the round: the done-word pass (after a list round its reports,
+    // if any, are few: one block) and the headers, without two more launches.  Every block's counts are
+    // device-scope atomics, released before its arrival is counted and acquired by the last block.
+    __shared__ uint32_t last_s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last_s = atomicAdd(sp.fin, 1u) == gridDim.x - 1u ? 1u : 0u;
     }
+    __syncthreads();
+    if (!last_s) return;
+    __threadfence();
+    if (x.dstat) done_out_body(a, x, 0u, 1u);
+    __syncthreads();
+    shard_pack_body(a, x, applied);
+    if (threadIdx.x == 0) *sp.fin = 0u;  // the next list round counts from 0 (stream order)
 }
 
 // Tallied round: place every receipt of F(r) into its bucket's segment, at this workgroup's
@@ -3201,8 +3245,8 @@ void launch_gs_full4x(const RoundArgs& a, const Xchg& x, const Launch& l) {
     hipLaunchKernelGGL(k_gs_full4x, dim3(l.grid), dim3(kBlock), 0, l.stream, a, x);
 }
 
-void launch_gs_sparse_x(const RoundArgs& a, const Xchg& x, const GsSparse& sp, const Launch& l) {
-    hipLaunchKernelGGL(k_gs_sparse_x, dim3(l.grid), dim3(kBlock), 0, l.stream, a, x, sp);
+void launch_gs_sparse_x(const RoundArgs& a, const Xchg& x, const GsSparse& sp, long long applied, const Launch& l) {
+    hipLaunchKernelGGL(k_gs_sparse_x, dim3(l.grid), dim3(kBlock), 0, l.stream, a, x, sp, applied);
 }
 
 void launch_shard_halo(const RoundArgs& a, const Xchg& x, int pushsum, hipStream_t s) {

@@ -7,6 +7,8 @@ rounds), and each round to a phase by the global completion count before it (the
     python3 tools/loop_phase_kernels.py KT_CSV SERIES_JSON ROUND_KERNEL [world] [warmup rounds, default 8] [bucket]
 
 ROUND_KERNEL: one name, or several separated by commas (full gossip's ramp: k_gs_sparse_x,k_gs_full4x).
+Warm-up rounds: the launches of run_local(max_rounds=8) per rank (gossip: 9, F(k) applies round k - 1).
+PER_ROUND=N (environment): also every kernel of the first N rounds, round by round.
 
 bucket: also the tail's rounds in buckets of that many (converged share, kernels and round kernel
 per rank-round).
@@ -14,6 +16,7 @@ per rank-round).
 import bisect
 import csv
 import json
+import os
 import statistics
 import sys
 from collections import defaultdict
@@ -67,6 +70,12 @@ def main():
         print(f"{label}: {len(rs)} rounds, kernels per rank-round {tot:.1f} us, per rank over these rounds {tot * len(rs) / 1e3:.2f} ms")
         for k in ks:
             print(f"  {k:48s} {statistics.fmean(per[r].get(k, 0.0) for r in rs) / world:9.2f} us")
+    per_round = int(os.environ.get("PER_ROUND", "0"))
+    if per_round:  # the first rounds one by one: every kernel's time per rank-round (us)
+        ks = sorted({k for r in per if r < per_round for k in per[r]})
+        print("round " + " ".join(f"{k[:16]:>16s}" for k in ks))
+        for r in sorted(x for x in per if x < per_round):
+            print(f"{r:5d} " + " ".join(f"{per[r].get(k, 0.0) / world:16.2f}" for k in ks))
     if bucket:
         tail = sorted(r for r in per if r < len(prev) and prev[r] * 100 >= 99 * nodes)
         print(f"tail by {bucket} rounds: rounds, not converged before, kernels / round kernel per rank-round (us)")
