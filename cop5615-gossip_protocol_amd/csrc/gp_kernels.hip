@@ -2281,6 +2281,8 @@ __global__ __launch_bounds__(kBlock) void k_gs_sparse(RoundArgs a, GsTally t, Gs
             atomicAdd(&a.inc_cur[u0], 1u);
             ++chains;
         }
+        // (every receipt listed, or only a first one by a returning atomic: C4 43.0-43.3 ms either way,
+        // profiles/round6/shard_ramp/c4_one_gpu_ab.txt)
         wave_append2(newh, v, sp.hl + hb, sp_ctr(sp, 1, r), size - hb, emit, u0, tcur, sp_ctr(sp, 2, r), size, sp.err);
     }
     if (r) block_add(newly, a.parts, (long long)r - 1);
