@@ -43,6 +43,12 @@ constexpr size_t kTallyThrDiv = GP_TALLY_THR_DIV;
 #ifndef GP_SPARSE_RAMP
 #define GP_SPARSE_RAMP 1  // A/B knob: full gossip's ramp on lists (k_gs_sparse), one GPU
 #endif
+#ifndef GP_SHARD_BINS
+#define GP_SHARD_BINS 1  // A/B knob: full gossip shards' receipt wave in bins (k_gs_bins_*)
+#endif
+#ifndef GP_BIN_DIV
+#define GP_BIN_DIV 16    // a round runs in bins when its receipts (estimated, every rank's) are >= actors / this
+#endif
 #ifndef GP_SHARD_RAMP
 #define GP_SHARD_RAMP 1  // A/B knob: the same on shards (k_gs_sparse_x)
 #endif
@@ -209,6 +215,7 @@ struct Handle {
     } gpl;
     int64_t bytes_sent = 0;        // exchange bytes this rank sent since the last reset (replays included)
     int64_t list_rounds = 0;       // full gossip: rounds run on the ramp's lists since the last reset
+    int64_t bin_rounds = 0;        // full gossip: rounds whose receipts went out in bins since the last reset
     const void* last_recv = nullptr;  // the receive buffer of the last gp_shard_deliver
     Ckpt ck;                       // activity tiers: the restore point (push-sum shards)
     int64_t full_until = 0;        // after a restore: the full plan until this many rounds are final
@@ -267,6 +274,11 @@ struct Handle {
     int64_t sp_until = 0;
     bool sp_frozen = false;
     bool sp_ran = false;          // a list round ran since the last sync (its error word is read there)
+    // full gossip shards: the receipt wave in bins (GsBins), decided per round with the
+    // round's plan (bin_next: the round gp_shard_round packs next), from values every rank holds
+    GsBins bins{};
+    bool bin_next = false;
+    int bin_state = 0;            // 0: no binned round yet, 1: binned rounds, 2: the wave is over
     int64_t sp_fused = -1;        // shards: the round whose list kernel also ran its done-word pass and pack
     int64_t sp_s = -1;            // the last synced holder count: sp_h holders (shards: every rank's)
     uint64_t sp_h = 1;            // after F(sp_s), which sizes a list round's grid
@@ -708,8 +720,11 @@ int reset(Handle* h) {
         h->last_recv = nullptr;
         h->bytes_sent = 0;
         h->list_rounds = 0;
+        h->bin_rounds = 0;
         if (h->kpiece > 1 && !h->full_out.empty()) use_layout(h, want_pieces(h));
         if (!h->full_out.empty()) full_plan(h);
+        h->bin_state = 0;
+        h->bin_next = false;
         if (gossip_plans(h) && !h->full_out.empty()) {
             // round 0's chains: the leader's one (program.fs:218); the sized plans run from round 0, so
             // the restore point is the initial state
@@ -845,6 +860,10 @@ void launch_main(Handle* h, int64_t k, const Xchg* x, bool timed, int piece = 0,
                 Launch ls = sp_launch(h, k, l);
                 ls.grid = std::min(ls.grid, kSpFusedGrid);  // (the last-block count: one atomic per block)
                 launch_gs_sparse_x(a, *x, h->gsp, h->gossip ? (long long)k - 1 : (long long)k, ls);
+            } else if (x && x->binned) {  // the receipt wave: counted, scanned, placed in bins
+                h->sp_frozen = true;
+                ++h->bin_rounds;
+                launch_gs_bins(a, *x, h->bins, h->stream);
             } else if (x) {
                 h->sp_frozen = true;
                 launch_gs_full4x(a, *x, l);
@@ -1335,6 +1354,7 @@ Xchg base_xchg(const Handle* h) {
     x.pstat = h->pstat;
     x.dship = h->dship;
     x.dstat = h->dstat;
+    x.binned = h->bin_next ? 1u : 0u;
     return x;
 }
 
@@ -1490,6 +1510,7 @@ int shard_deliver(Handle* h, const void* recv) {
         const GsSparse sp = h->gsp.hl && !h->sp_frozen ? h->gsp : GsSparse{};
         launch_shard_unpack(h->args((uint32_t)k), x, applied_round(h, k), most, h->gossip ? 1 : 0, h->full ? 1 : 0, sp,
                             h->stream);
+        if (x.binned) launch_shard_unpack_bins(h->args((uint32_t)k), x, h->bins, h->stream);  // the receipts in bins
     }
     HIP_TRY(hipGetLastError());
     h->awaiting_deliver = false;
@@ -1577,15 +1598,43 @@ uint32_t gs_dpairs(const Handle* h, int p, uint32_t dw) {
     return 2u * d >= nw ? 0u : (uint32_t)d;
 }
 
+// Whether round k's receipts travel in bins (GsBins): while the round's receipts, estimated from the
+// synced values every rank holds (the chain bound of gs_cap times the share of nodes not done), are at
+// least actors / GP_BIN_DIV, once per run (the wave); never in a list round (GP_FLAG_GOSSIP_TALLY: every
+// other round from round 1, a test hook).
+bool bins_round(Handle* h, int64_t k) {
+    if (!h->bins.cnt || k < 1) return false;
+    if (h->gsp.hl && !h->sp_frozen && k < h->sp_until) return false;
+    if (h->cfg.flags & GP_FLAG_GOSSIP_TALLY) return true;
+    if (h->bin_state == 2) return false;
+    const Handle::GossipPlan& P = h->gpl;
+    const double A = (double)h->g.actors, n = (double)h->lay.nodes;
+    const int64_t dk = std::max<int64_t>(k - P.j, 0);
+    const double cb = dk >= 62 ? A : std::min(A, P.cj * std::ldexp(1.0, (int)dk));
+    const bool on = cb * ((n - (double)h->completed) / n) * GP_BIN_DIV >= A;
+    if (on) h->bin_state = 1;
+    else if (h->bin_state == 1) h->bin_state = 2;
+    return on;
+}
+
+uint32_t bins_of(const Handle* h, int q) {
+    return (uint32_t)((h->abnd[q + 1] - h->abnd[q] + (1 << kTallyShift) - 1) >> kTallyShift);
+}
+
 // Round k's plan (k = the next round gp_shard_round packs).
 void gossip_round_plan(Handle* h, int64_t k) {
     const int W = h->world, p = h->rank;
     const Handle::GossipPlan& P = h->gpl;
+    h->bin_next = bins_round(h, k);
     std::vector<uint32_t> oc((size_t)W, 0u), ic((size_t)W, 0u), od((size_t)W, 0u), id((size_t)W, 0u);
     for (int q = 0; q < W; ++q) {
         if (q == p) continue;
         oc[q] = gs_cap(h, p, q, k, P.seen ? P.m_out[q] : 0u, h->full_out[q].cap);
         ic[q] = gs_cap(h, q, p, k, P.seen ? P.m_in[q] : 0u, h->full_in[q].cap);
+        if (h->bin_next) {  // u16 entries: half the words, and the receiver's bin starts beside them
+            oc[q] = (oc[q] + 1) / 2 + (bins_of(h, q) + kSub) / kSub;
+            ic[q] = (ic[q] + 1) / 2 + (bins_of(h, p) + kSub) / kSub;
+        }
         od[q] = gs_dpairs(h, p, P.seen ? P.dw_out : 0u);
         id[q] = gs_dpairs(h, q, P.seen ? P.dw_in[q] : 0u);
     }
@@ -1708,6 +1757,7 @@ int restore(Handle* h, int64_t reached) {
     // the restore point holds the arrays, not the ramp's lists: the replay walks every actor
     h->sp_frozen = true;
     h->sp_fused = -1;
+    h->bin_next = false;  // (the full plan's first round runs in entries; the next plans decide again)
     h->rounds = c.rounds;
     h->completed = c.completed;
     h->converged = false;
@@ -2094,6 +2144,25 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
                     sp.fin = sp.ctr + 3 * 4 * kSpStride;  // (its own line, after the counters)
                     if (hipHostMalloc((void**)&h->h_spctr, (3 * 4 * kSpStride + 1) * sizeof(uint32_t)) != hipSuccess)
                         return bail(fail(GP_ENOMEM, "hipHostMalloc failed"));
+                }
+            }
+            // full gossip shards: the receipt wave in bins (the passes' counters and their scan)
+            if (GP_SHARD_BINS && gossip_plans(h) && prepare_gs_bins() == 0) {
+                GsBins& b = h->bins;
+                uint32_t nbt = 0;
+                for (int q = 0; q < h->world; ++q) {
+                    b.bin0[q] = nbt;
+                    if (q != h->rank) nbt += bins_of(h, q);
+                }
+                b.bin0[h->world] = nbt;
+                b.nbt = nbt;
+                b.nb_self = bins_of(h, h->rank);
+                b.W = (uint32_t)std::min(grid_for((uint32_t)n), 1024);
+                const size_t nc = (size_t)nbt * b.W;
+                if (nbt && nbt <= kMaxBins && nc < (1u << 31)) {
+                    if ((rc = h->alloc(&b.cnt, nc)) || (rc = h->alloc(&b.off, nc + 1)) ||
+                        (rc = h->alloc(&b.scratch, scan_scratch_words((uint32_t)nc))))
+                        return bail(rc);
                 }
             }
         } else if ((rc = h->alloc(&h->dir[0], xn, xlo)) || (rc = h->alloc(&h->dir[1], xn, xlo))) {
@@ -2848,6 +2917,7 @@ int gp_shard_stats(void* handle, gp_shard_counters* out) {
     out->restore_round = h->ck.valid ? h->ck.rounds : -1;
     out->bytes_sent = h->bytes_sent;
     out->list_rounds = h->list_rounds;
+    out->bin_rounds = h->bin_rounds;
     return GP_OK;
 }
 

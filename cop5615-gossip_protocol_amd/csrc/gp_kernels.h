@@ -167,6 +167,7 @@ struct ShardHeader {
                                // the words were written, 0 when no word changed
     uint32_t dwant;            // the sender's own done words that differed from what it had shipped
                                // (before the pair capacity): both ends size the next done parts from it
+    uint32_t binned;           // full gossip: the receipts travel in bins (GsBins below), not as entries
 };
 static_assert(sizeof(ShardHeader) <= 256, "the chunk header is 256 bytes");
 
@@ -225,6 +226,7 @@ struct Xchg {
     uint32_t* pstat;                  // [kPstatWords] the plan inputs of the last round (-> host; kPs*)
     uint32_t* dship;                  // own done words as last shipped (global word index)
     uint32_t* dstat;                  // [kDstatWords]: dirty-word counter, backlog flag
+    uint32_t binned;                  // full gossip: this round's receipts travel in bins (GsBins)
     PeerOut out[kMaxWorld];
     PeerIn in[kMaxWorld];
     HaloX h;
@@ -337,6 +339,29 @@ void launch_shard_done_out(const RoundArgs& a, const Xchg& x, hipStream_t s);
 // the scan, scatter and tally passes of a tallied round (each exits at once otherwise)
 void launch_gs_tally(const RoundArgs& a, const GsTally& t, const Launch& l);
 int prepare_gs_tally();  // once per process: allow the tally pass's 128 KB of dynamic LDS (0: ok)
+// Full gossip on shards, the receipt wave: the remote receipts of a round travel
+// binned by target, bin b of peer q holding q's actors [abnd[q] + b * 2^kTallyShift, ...).  F(k)
+// (k_gs_bins_count) counts them per (peer, bin) and workgroup in LDS, an exclusive scan gives every
+// (peer, bin, workgroup) its place, and k_gs_bins_place draws the same receipts again into their places,
+// as u16 offsets in the bin.  The chunk's entry part then holds the bins' starts (nb + 1 u32 words,
+// nb = the receiver's bins) and the u16 entries.  The receiver counts a bin per workgroup in LDS and
+// adds the counts to its receipt words (k_shard_unpack_bins): no fabric atomics, 2 bytes a receipt.
+// No sender-side done filter in these rounds: F(k + 1) drops the receipts of done actors itself.
+struct GsBins {
+    uint32_t* cnt;                 // [nbt][W]: receipts per (peer, bin) and workgroup (tally_col order)
+    uint32_t* off;                 // its exclusive scan, nbt * W + 1 words
+    uint32_t* scratch;             // the scan's scratch
+    uint32_t W;                    // grid of k_gs_bins_count / k_gs_bins_place (a multiple of 8)
+    uint32_t nbt;                  // bins over every peer
+    uint32_t nb_self;              // bins of this rank's range (the receiver's grid)
+    uint32_t bin0[kMaxWorld + 1];  // first bin of each peer (this rank: none), bin0[world] = nbt
+};
+constexpr uint32_t kMaxBins = 8192;  // the passes' LDS counters (u32 per bin)
+int prepare_gs_bins();               // once per process: the receiver's 128 KB of dynamic LDS (0: ok)
+// F(k) in bins: k_gs_bins_count, the scan, k_gs_bins_place (the chunks' entry parts)
+void launch_gs_bins(const RoundArgs& a, const Xchg& x, const GsBins& b, hipStream_t s);
+// after the exchange: every peer's bins of this rank into inc_cur (one workgroup per bin)
+void launch_shard_unpack_bins(const RoundArgs& a, const Xchg& x, const GsBins& b, hipStream_t s);
 // sharded variants: remote link / full-topology messages go to the send chunks of x
 void launch_ps_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);
 void launch_gs_link_scatter_x(const RoundArgs& a, const Xchg& x, const Launch& l);

@@ -1423,6 +1423,7 @@ __device__ __forceinline__ void shard_pack_body(const RoundArgs& a, const Xchg& 
         x.pmax[q] = m;
         hd->runmax = m;
         hd->chains = (uint32_t)chains_s;
+        hd->binned = x.binned;
         // the done part: pairs written (capped), or whether the whole words were written
         const uint32_t dp = x.out[q].dpairs;
         hd->ndone = !x.out[q].done ? 0u : dp ? (dirty_s < dp ? dirty_s : dp) : (dirty_s ? 1u : 0u);
@@ -1574,7 +1575,8 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(RoundArgs a, Xchg x, lo
     // flight together (one peer after another left each thread a chain of dependent loads per peer)
     const uint32_t bpp = gridDim.x / x.world;
     const uint32_t q = blockIdx.x / bpp;
-    if (q < x.world && q != x.rank && x.in[q].cap && (blockIdx.x % bpp) * kBlock + threadIdx.x < kSub * x.in[q].cap) {
+    if (q < x.world && q != x.rank && x.in[q].cap && (blockIdx.x % bpp) * kBlock + threadIdx.x < kSub * x.in[q].cap &&
+        !(full && x.in[q].hdr->binned)) {  // (binned receipts: k_shard_unpack_bins)
         const PeerIn& in = x.in[q];
         // kSub sub-segments of `cap` entries, each walked up to its count only (a chunk sized for an
         // all-sending round holds a few entries in most rounds)
@@ -2399,6 +2401,211 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
         __syncthreads();  // block_add's LDS slots are reused
         block_add(chains, a.cparts, r);
     }
+}
+
+// ---- full gossip on shards: the receipt wave in bins (GsBins, gp_kernels.h)
+// Owner rank qq of remote target u and its bin in the passes' numbering: one uniform loop over the
+// ranks (scalar loads and selects; a per-lane index into the kernel arguments is a vector load per
+// receipt, which kept the texture path 88% busy).
+__device__ __forceinline__ void peer_bin(const Xchg& x, const GsBins& b, uint32_t u, uint32_t& qq, uint32_t& bin) {
+    uint32_t q = 0, base = x.abnd[0], b0 = b.bin0[0];
+    for (uint32_t i = 1; i < x.world; ++i) {
+        const bool ge = u >= x.abnd[i];
+        q = ge ? i : q;
+        base = ge ? x.abnd[i] : base;
+        b0 = ge ? b.bin0[i] : b0;
+    }
+    qq = q;
+    bin = b0 + ((u - base) >> kTallyShift);
+}
+// A chunk's entry part in bins: the start table (nb + 1 words), then the u16 entries (their capacity).
+__device__ __forceinline__ uint32_t bins_room(uint32_t cap, uint32_t nb) {
+    const uint32_t w = kSub * cap;
+    return w > nb + 1u ? 2u * (w - nb - 1u) : 0u;
+}
+
+// F(r) of a receipt-wave round: k_gs_full4x's walk, apply and draws; a local receipt is an atomic as
+// there, a remote one is counted in its (peer, bin) LDS counter, written out per workgroup for the scan.
+// Every receipt is sent (no sender-side filter: a bin entry costs less than the filter's bitmap read).
+__global__ __launch_bounds__(kBlock) void k_gs_bins_count(RoundArgs a, Xchg x, GsBins b) {
+    extern __shared__ uint32_t lc[];
+    const uint32_t r = a.r;
+    if (a.cparts && blockIdx.x == 0 && threadIdx.x < 64) *part_slot(a.cparts, r + 2u, threadIdx.x) = 0u;
+    for (uint32_t i = threadIdx.x; i < b.nbt; i += kBlock) lc[i] = 0u;
+    unsigned long long prev = 0;
+    if (r) prev = gate_count(a, (long long)r - 1);
+    const bool live = !(r && prev >= a.target);  // converged: zero counts still go out (no entry placed)
+    const bool deep = deep_tail(prev, a.target);
+    __syncthreads();
+    const uint32_t lo = a.lo, hi = a.hi;
+    const uint32_t q0 = (lo >> 2) & ~7u, q1 = (hi + 3u) >> 2, nq = q1 - q0;
+    const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;
+    uint32_t q, end, step;
+    node_range(q0, q1, span4, q, end, step);
+    if (!live) end = 0;
+    uint32_t newly = 0, chains = 0;
+    // block-uniform trip count (the done word's shuffles); lanes past the end idle
+    for (; q - threadIdx.x < end; q += step) {
+        const bool valid = q < end;
+        const uint32_t v0 = q << 2;
+        uint32_t st4 = 0, done4 = 0, mine = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) mine |= (valid && v0 + j - lo < hi - lo) ? 1u << j : 0u;
+        if (mine) {
+            bool due;
+            uint4 in4 = load_quad(a, nullptr, v0, r, deep, st4, due);
+            uint32_t inc[4] = {in4.x, in4.y, in4.z, in4.w};
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                if (!((mine >> j) & 1u)) inc[j] = 0u;
+            if (inc[0] | inc[1] | inc[2] | inc[3]) st4 = gs_apply4(a, v0, st4, inc, true, done4, newly);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t v = v0 + j, tok = ((mine >> j) & 1u) ? (st4 >> (8u * j)) & 3u : 0u;
+                if (!tok) continue;
+                chains += tok;
+                const uint4 px = philox(v, r, kStreamGossip, a.seed);  // program.fs:89-95
+                const uint32_t t0 = scale_draw(px.x, a.nodes), t1 = scale_draw(px.y, a.nodes);
+                const uint32_t u[2] = {t0 + (t0 >= v ? 1u : 0u), t1 + (t1 >= v ? 1u : 0u)};
+#pragma unroll
+                for (uint32_t c = 0; c < 2; ++c) {
+                    if (tok <= c) break;
+                    if (u[c] - lo < hi - lo) {
+                        atomicAdd(&a.inc_cur[u[c]], 1u);
+                    } else {
+                        uint32_t qq, bin;
+                        peer_bin(x, b, u[c], qq, bin);
+                        atomicAdd(&lc[bin], 1u);
+                    }
+                }
+            }
+        }
+        // the reports of this round into the done bitmap: 8 lanes = 32 actors = one word
+        uint32_t w = done4 << ((q & 7u) * 4u);
+        w |= __shfl_xor(w, 1, 64);
+        w |= __shfl_xor(w, 2, 64);
+        w |= __shfl_xor(w, 4, 64);
+        if (w && (q & 7u) == 0u) {
+            const uint32_t wi = q >> 3;
+            if (a.dsum) {
+                const uint32_t old = atomicOr(&a.dbits[wi], w);
+                if ((old | w) == ~0u && old != ~0u) atomicOr(&a.dsum[wi >> 5], 1u << (wi & 31u));
+            } else {
+                atomicOr(&a.dbits[wi], w);
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t col = tally_col(blockIdx.x, b.W);
+    for (uint32_t i = threadIdx.x; i < b.nbt; i += kBlock) b.cnt[i * b.W + col] = lc[i];
+    if (r) block_add(newly, a.parts, (long long)r - 1);
+    if (a.cparts) {
+        __syncthreads();  // block_add's LDS slots are reused
+        block_add(chains, a.cparts, r);
+    }
+}
+
+// The placement of a receipt-wave round: the same grid and walk as k_gs_bins_count, the same draws
+// from the states F(r) left, so every (peer, bin, workgroup) gets exactly the count it reported; a
+// receipt takes the next place of its (peer, bin) in LDS.  Block 0 writes every peer's bin starts and
+// sets the entry counters the pack reports (its total over the sub-segments, within each one's
+// capacity); a chunk whose entries outgrow its room overflows (replayed or fatal, as entries).
+__global__ __launch_bounds__(kBlock) void k_gs_bins_place(RoundArgs a, Xchg x, GsBins b) {
+    extern __shared__ uint32_t lp[];
+    __shared__ uint32_t pbase[kMaxWorld], proom[kMaxWorld], pabnd[kMaxWorld];
+    __shared__ uint16_t* pe16[kMaxWorld];
+    const uint32_t r = a.r;
+    unsigned long long prev = 0;
+    if (r) prev = gate_count(a, (long long)r - 1);
+    const bool live = !(r && prev >= a.target);
+    const uint32_t col = tally_col(blockIdx.x, b.W);
+    for (uint32_t i = threadIdx.x; i < b.nbt; i += kBlock) lp[i] = b.off[i * b.W + col];
+    if (threadIdx.x < x.world) {  // per peer: first entry, room, first actor, entries (LDS: per-lane reads)
+        const uint32_t qq = threadIdx.x, nb = b.bin0[qq + 1u] - b.bin0[qq];
+        pbase[qq] = b.off[b.bin0[qq] * b.W];
+        proom[qq] = qq == x.rank ? 0u : bins_room(x.out[qq].cap, nb);
+        pabnd[qq] = x.abnd[qq];
+        pe16[qq] = qq == x.rank ? nullptr : reinterpret_cast<uint16_t*>(x.out[qq].slot + nb + 1u);
+    }
+    __syncthreads();
+    if (blockIdx.x == 0) {  // the bin starts, relative to each peer's first entry
+        for (uint32_t qq = 0; qq < x.world; ++qq) {
+            if (qq == x.rank) continue;
+            const uint32_t nb = b.bin0[qq + 1u] - b.bin0[qq];
+            for (uint32_t i = threadIdx.x; i <= nb; i += kBlock) x.out[qq].slot[i] = b.off[(b.bin0[qq] + i) * b.W] - pbase[qq];
+            if (threadIdx.x < kSub) {
+                const uint32_t e = b.off[b.bin0[qq + 1u] * b.W] - pbase[qq], cap = x.out[qq].cap;
+                const uint32_t per = (e + kSub - 1u) / kSub;
+                *ctr_at(x, qq, threadIdx.x) = per < cap ? per : cap;
+                if (threadIdx.x == 0 && e > bins_room(cap, nb)) atomicOr(x.overflow, 1u);
+            }
+        }
+    }
+    if (!live) return;
+    const uint32_t lo = a.lo, hi = a.hi;
+    const uint32_t q0 = (lo >> 2) & ~7u, q1 = (hi + 3u) >> 2, nq = q1 - q0;
+    const uint32_t span4 = (((nq + 7u) >> 3) + kBlock - 1u) / kBlock * kBlock;
+    uint32_t q, end, step;
+    node_range(q0, q1, span4, q, end, step);
+    for (; q < end; q += step) {
+        const uint32_t v0 = q << 2;
+        uint32_t mine = 0;  // (as k_gs_bins_count: a quad with none of this rank's actors is not read)
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) mine |= v0 + j - lo < hi - lo ? 1u << j : 0u;
+        if (!mine) continue;
+        const uint32_t st4 = *reinterpret_cast<const uint32_t*>(a.gstate + v0);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t v = v0 + j;
+            const uint32_t tok = ((mine >> j) & 1u) ? (st4 >> (8u * j)) & 3u : 0u;
+            if (!tok) continue;
+            const uint4 px = philox(v, r, kStreamGossip, a.seed);
+            const uint32_t t0 = scale_draw(px.x, a.nodes), t1 = scale_draw(px.y, a.nodes);
+            const uint32_t u[2] = {t0 + (t0 >= v ? 1u : 0u), t1 + (t1 >= v ? 1u : 0u)};
+#pragma unroll
+            for (uint32_t c = 0; c < 2; ++c) {
+                if (tok <= c) break;
+                if (u[c] - lo < hi - lo) continue;  // local: added by F(r)
+                uint32_t qq, bin;
+                peer_bin(x, b, u[c], qq, bin);
+                const uint32_t pos = atomicAdd(&lp[bin], 1u) - pbase[qq];
+                if (pos < proom[qq]) pe16[qq][pos] = (uint16_t)((u[c] - pabnd[qq]) & ((1u << kTallyShift) - 1u));
+            }
+        }
+    }
+}
+
+// The receiver of a receipt-wave round: workgroup = one bin of this rank's actors; every peer's entries
+// of the bin counted in LDS, then added to the receipt words (local receipts are already there).  A
+// done actor's receipts are added too: F(r + 1) ignores them (program.fs:92's filter, at the receiver).
+constexpr uint32_t kBinBlock = 1024;
+__global__ __launch_bounds__(kBinBlock) void k_shard_unpack_bins(RoundArgs a, Xchg x, GsBins b) {
+    extern __shared__ uint32_t h[];
+    constexpr uint32_t S = 1u << kTallyShift;
+    for (uint32_t i = threadIdx.x; i < S; i += kBinBlock) h[i] = 0u;
+    __syncthreads();
+    const uint32_t bin = blockIdx.x, nb = b.nb_self;
+    const uint32_t base = x.abnd[x.rank] + (bin << kTallyShift), top = x.abnd[x.rank + 1u];
+    const uint32_t n = top - base < S ? top - base : S;
+    for (uint32_t qq = 0; qq < x.world; ++qq) {
+        const PeerIn& in = x.in[qq];
+        if (qq == x.rank || !in.cap || !in.hdr->binned) continue;  // uniform
+        const uint32_t room = bins_room(in.cap, nb), e = in.slot[nb];
+        const uint32_t s0 = in.slot[bin], s1 = min(in.slot[bin + 1u], min(e, room));
+        if (s0 > s1) {  // a corrupt chunk: reported, never applied
+            if (threadIdx.x == 0 && s0 > in.slot[bin + 1u]) atomicOr(x.overflow, 2u);
+            continue;
+        }
+        const uint16_t* e16 = reinterpret_cast<const uint16_t*>(in.slot + nb + 1u);
+        for (uint32_t i = s0 + threadIdx.x; i < s1; i += kBinBlock) {
+            const uint32_t t = e16[i];
+            if (t < n) atomicAdd(&h[t], 1u);
+            else atomicOr(x.overflow, 2u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += kBinBlock)
+        if (const uint32_t c = h[i]) a.inc_cur[base + i] += c;
 }
 
 // Positions of one entry per thread in peer q's chunk, sub-segment sb (both per thread): LDS counters
@@ -3245,6 +3452,28 @@ void launch_shard_done_out(const RoundArgs& a, const Xchg& x, hipStream_t s) {
 
 void launch_gs_full4x(const RoundArgs& a, const Xchg& x, const Launch& l) {
     hipLaunchKernelGGL(k_gs_full4x, dim3(l.grid), dim3(kBlock), 0, l.stream, a, x);
+}
+
+int prepare_gs_bins() {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_shard_unpack_bins), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)((1u << kTallyShift) * sizeof(uint32_t))) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    return 0;
+}
+
+void launch_gs_bins(const RoundArgs& a, const Xchg& x, const GsBins& b, hipStream_t s) {
+    const unsigned lds = b.nbt * (unsigned)sizeof(uint32_t);
+    hipLaunchKernelGGL(k_gs_bins_count, dim3(b.W), dim3(kBlock), lds, s, a, x, b);
+    launch_exclusive_scan(b.cnt, b.off, b.nbt * b.W, b.scratch, s);
+    hipLaunchKernelGGL(k_gs_bins_place, dim3(b.W), dim3(kBlock), lds, s, a, x, b);
+}
+
+void launch_shard_unpack_bins(const RoundArgs& a, const Xchg& x, const GsBins& b, hipStream_t s) {
+    if (!b.nb_self) return;
+    hipLaunchKernelGGL(k_shard_unpack_bins, dim3(b.nb_self), dim3(kBinBlock), (1u << kTallyShift) * (unsigned)sizeof(uint32_t),
+                       s, a, x, b);
 }
 
 void launch_gs_sparse_x(const RoundArgs& a, const Xchg& x, const GsSparse& sp, long long applied, const Launch& l) {

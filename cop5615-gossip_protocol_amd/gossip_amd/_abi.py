@@ -65,7 +65,7 @@ class ShardLayout(C.Structure):
 class ShardStats(C.Structure):
     _fields_ = [("plan_changes", C.c_int64), ("restores", C.c_int64), ("send_bytes", C.c_int64),
                 ("recv_bytes", C.c_int64), ("restore_round", C.c_int64), ("bytes_sent", C.c_int64),
-                ("list_rounds", C.c_int64)]
+                ("list_rounds", C.c_int64), ("bin_rounds", C.c_int64)]
 
 
 EXPORTS = ["gp_abi_version", "gp_sizes", "gp_create", "gp_reset", "gp_step", "gp_read_gossip",

@@ -48,13 +48,14 @@ class HipShard:
                  device: int = 0, stream: int | None = None, kernel_timing: bool = False, delta: float = 1e-10,
                  gossip_threshold: int = 10, term_init: int = 1, term_limit: int = 3, quiet_waves: bool = False,
                  full_plan: bool = False, tight_tiers: bool = False, pieces: bool = True,
-                 force_pieces: bool = False):
+                 force_pieces: bool = False, force_bins: bool = False):
         """quiet_waves: the push-sum quiet-tail walk at any shard size (a test hook; on by default
         for shards of 2^20 actors or more).  full_plan: no activity tiers (every round ships the
         all-sending capacity); tight_tiers: tiers with no headroom and frequent replays (a test
         hook).  pieces: exchange a push-sum round piece by piece (the library picks 4 pieces from
         2^25 actors per rank until half the nodes have converged, else 1); force_pieces: 4 pieces
-        at any size (a test hook)."""
+        at any size (a test hook).  force_bins: full gossip sends its receipts in bins in every round
+        past the ramp's lists (by default the receipt wave only; a test hook)."""
         import torch
 
         if topology not in _abi.TOPOLOGIES:
@@ -68,6 +69,7 @@ class HipShard:
         flags |= _abi.FLAG_QUIET_WAVES if quiet_waves else 0
         flags |= (_abi.FLAG_FULL_PLAN if full_plan else 0) | (_abi.FLAG_TIGHT_TIERS if tight_tiers else 0)
         flags |= (_abi.FLAG_PIECES if pieces or force_pieces else 0) | (_abi.FLAG_FORCE_PIECES if force_pieces else 0)
+        flags |= _abi.FLAG_GOSSIP_TALLY if force_bins else 0
         if stream is None:
             stream = torch.cuda.current_stream(device).cuda_stream
         self.cfg = _abi.Config(n_arg, _abi.TOPOLOGIES[topology], _abi.ALGOS[algorithm], seed, delta,
@@ -137,7 +139,7 @@ class HipShard:
         _abi.check(self.lib.gp_shard_stats(self.h, C.byref(s)))
         return {"plan_changes": s.plan_changes, "restores": s.restores, "send_bytes": s.send_bytes,
                 "recv_bytes": s.recv_bytes, "restore_round": s.restore_round, "bytes_sent": s.bytes_sent,
-                "list_rounds": s.list_rounds}
+                "list_rounds": s.list_rounds, "bin_rounds": s.bin_rounds}
 
     @property
     def nodes(self) -> int:

@@ -53,7 +53,10 @@ enum gp_flags {
                                   size (default: from 2^20 actors on); a test hook, same results */
     GP_FLAG_GOSSIP_TALLY = 64, /* full gossip, one GPU: tally receipts by target bucket in every
                                   round from round 1 at any graph size (default: from 2^20 actors,
-                                  after a round with many chains); a test hook, same results */
+                                  after a round with many chains); full-gossip shards (ABI 8): send
+                                  the receipts in bins in every round from round 1 that does not
+                                  run on the ramp's lists (default: the receipt wave); a test hook,
+                                  same results */
     GP_FLAG_FULL_PLAN = 128,   /* push-sum and full-gossip shards: keep the full exchange plan (no
                                   activity tiers, no per-round plans) */
     GP_FLAG_TIGHT_TIERS = 256, /* push-sum and full-gossip shards: sized plans from the first batch
@@ -245,6 +248,8 @@ typedef struct gp_shard_counters {
                                rounds packed (replayed rounds included) (ABI 6)                  */
     int64_t list_rounds;    /* full gossip: rounds this rank ran on its ramp lists since the last
                                reset (ABI 8)                                                     */
+    int64_t bin_rounds;     /* full gossip: rounds whose receipts this rank sent in bins since the
+                               last reset (ABI 8)                                                */
 } gp_shard_counters;
 /* Exchange-plan counters of a shard (num_gpus > 1 handle: rank 0's). */
 int gp_shard_stats(void* handle, gp_shard_counters* out);

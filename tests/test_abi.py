@@ -89,15 +89,16 @@ def test_kstats_struct_layout():
 
 def test_shard_counters_struct_layout():
     """gp_shard_counters (ABI 5: activity tiers of the shard exchange; ABI 6 appended bytes_sent, ABI 8
-    list_rounds) as the header lays it out."""
+    list_rounds and bin_rounds) as the header lays it out."""
     import ctypes as C
 
     text = open(_abi.HEADER).read()
     body = re.search(r"typedef struct gp_shard_counters \{(.*?)\} gp_shard_counters;", text, re.S).group(1)
     names = re.findall(r"^\s*int64_t\s+(\w+)", body, re.M)
     assert names == [f[0] for f in _abi.ShardStats._fields_] == [
-        "plan_changes", "restores", "send_bytes", "recv_bytes", "restore_round", "bytes_sent", "list_rounds"]
-    assert C.sizeof(_abi.ShardStats) == 56
+        "plan_changes", "restores", "send_bytes", "recv_bytes", "restore_round", "bytes_sent", "list_rounds",
+        "bin_rounds"]
+    assert C.sizeof(_abi.ShardStats) == 64
 
 
 def test_config_struct_layout():

@@ -348,6 +348,56 @@ def test_full_gossip_shard_ramp_lists_vs_oracle(n, world, seed):
         e.close()
 
 
+@pytest.mark.parametrize("tiers", ["default", "tight", "full"])
+@pytest.mark.parametrize("n,world,seed", [(1000, 2, 2), (20000, 3, 4), (100000, 8, 5), (300000, 5, 8)])
+def test_full_gossip_shard_bins_vs_oracle(n, world, seed, tiers):
+    """Full gossip's receipts in bins on shards (k_gs_bins_count / k_gs_bins_place / k_shard_unpack_bins,
+    DESIGN.md §6.15), forced in every round after the ramp's lists: the sender counts each (peer, bin)
+    per workgroup, places u16 offsets after a scan, and the receiver counts a bin per workgroup and adds
+    to its receipt words.  No sender-side filter in these rounds.  With the three plans (per-round,
+    tight: overflowed batches replay from restore points, full), stopped at several rounds, bit-exact
+    against the oracle, twice (after a reset)."""
+    kw = {"tight_tiers": True} if tiers == "tight" else {"full_plan": True} if tiers == "full" else {}
+    engines = _shards(n, "full", "gossip", world, seed, force_bins=True, **kw)
+    for rep in range(2):
+        ref = oracle.OracleSim(n, "full", "gossip", seed=seed)
+        if rep:
+            for e in engines:
+                e.reset()
+        for chunk in (3, 5, 8, 13, 1 << 20):
+            rs = ref.step(chunk, threads=8)
+            sts = sharded.run_local(engines, max_rounds=int(rs.round) - int(engines[0].status.round))
+            for st in sts:
+                assert (st.round, st.completed, st.converged) == (rs.round, rs.completed, rs.converged)
+            _check_vs(ref, engines, "gossip")
+            if rs.converged:
+                break
+        assert rs.converged
+        ss = [e.shard_stats() for e in engines]
+        assert all(x["bin_rounds"] > 0 for x in ss), ss
+    for e in engines:
+        e.close()
+
+
+def test_full_gossip_shard_bins_default_wave():
+    """Without the test hook the receipt wave runs in bins (the chain bound times the share of nodes not
+    done at least actors / 16), the ramp on lists before it and entries with the sender filter after it:
+    all three kinds of rounds in one run at 2M actors on 8 ranks, bit-exact against the single-GPU engine."""
+    n, world, seed = 2_000_000, 8, 3
+    ref = Simulator(n, "full", "gossip", seed=seed)
+    rs = ref.step()
+    engines = _shards(n, "full", "gossip", world, seed)
+    sts = sharded.run_local(engines)
+    assert (sts[0].round, sts[0].completed, sts[0].converged) == (rs.round, rs.completed, rs.converged)
+    _check_vs(ref, engines, "gossip")
+    ss = [e.shard_stats() for e in engines]
+    assert len({(x["bin_rounds"], x["list_rounds"]) for x in ss}) == 1, ss
+    lr, br = ss[0]["list_rounds"], ss[0]["bin_rounds"]
+    assert lr > 0 and br > 0 and lr + br + 1 < int(rs.round), (lr, br, int(rs.round))
+    for e in engines:
+        e.close()
+
+
 @pytest.mark.parametrize("n,topo,world,seed", [(20000, "Imp3D", 3, 5), (300000, "Imp3D", 8, 11)])
 def test_group_tight_tiers_vs_oracle(n, topo, world, seed):
     """The library's multi-GPU engine (gp_step over num_gpus shards, here on one device) with

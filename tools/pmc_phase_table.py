@@ -39,9 +39,10 @@ def load(d):
 def rounds_of(disp, rk, world, warmup):
     """dispatch id -> round (None before the first real round)."""
     seen, rnd, out = 0, -1, {}
+    rks = rk.split(",")  # (full gossip shards: the ramp's, the receipt wave's and the dense round kernels)
     for did in sorted(disp):
         k = disp[did][0]
-        if k == rk or k.startswith(rk + "<"):  # (k_ps_quiet_x<false> / <true>)
+        if any(k == x or k.startswith(x + "<") for x in rks):  # (k_ps_quiet_x<false> / <true>)
             rnd = seen // world - warmup
             seen += 1
         out[did] = rnd if rnd >= 0 else None
