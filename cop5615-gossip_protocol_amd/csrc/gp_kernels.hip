@@ -197,6 +197,41 @@ __device__ __forceinline__ void put(const Xchg& x, uint32_t q, uint32_t pos, uin
     }
 }
 
+// The peers' send chunks in LDS, filled by the block's reservation (block_reserve / block_reserve_qs)
+// before its first barrier: put_t reads a lane's peer there.  (put indexes the kernel arguments by a
+// per-lane peer, one vector load per field and entry, which keeps the texture path busy.)
+struct PeerTab {
+    uint32_t* slot[kMaxWorld];
+    double2* msg[kMaxWorld];
+    uint32_t cap[kMaxWorld];
+};
+__device__ __forceinline__ PeerTab& peer_tab() {
+    __shared__ PeerTab t;
+    return t;
+}
+__device__ __forceinline__ void peer_tab_fill(const Xchg& x) {
+    if (threadIdx.x < kMaxWorld) {
+        PeerTab& t = peer_tab();
+        const PeerOut& o = x.out[threadIdx.x];
+        t.slot[threadIdx.x] = o.slot;
+        t.msg[threadIdx.x] = o.msg;
+        t.cap[threadIdx.x] = o.cap;
+    }
+}
+template <bool MSG>
+__device__ __forceinline__ void put_t(const Xchg& x, uint32_t q, uint32_t pos, uint32_t entry, double2 m,
+                                      uint32_t sub = kSub) {
+    const PeerTab& t = peer_tab();
+    const uint32_t cap = t.cap[q];
+    if (pos < cap) {
+        const uint32_t i = (sub < kSub ? sub : my_sub()) * cap + pos;
+        t.slot[q][i] = entry;
+        if (MSG) t.msg[q][i] = m;
+    } else {
+        atomicOr(x.overflow, 1u);
+    }
+}
+
 // Wave-level reservation for one entry per lane (lanes with want): one atomic per peer present on
 // the sub-segment counter of peer q (the quiet-tail rounds of a shard, where entries are few and the
 // walk is per wave).  Every lane of the wave must call it.
@@ -1219,6 +1254,7 @@ __device__ __forceinline__ void block_reserve(const Xchg& x, const bool (&want)[
     if (sub >= kSub) sub = my_sub();
     __shared__ uint32_t cnt[kMaxWorld], base[kMaxWorld];
     if (threadIdx.x < kMaxWorld) cnt[threadIdx.x] = 0u;
+    peer_tab_fill(x);
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < K; ++j) pos[j] = want[j] ? atomicAdd(&cnt[q[j]], 1u) : 0u;
@@ -1234,7 +1270,10 @@ __device__ __forceinline__ void block_reserve(const Xchg& x, const bool (&want)[
 
 // Actors per thread of the sharded link passes (block-strided): more per block means fewer
 // block-level reservations (three barriers and one global atomic per peer each).
-constexpr uint32_t kShardPer = 4;
+#ifndef GP_SHARD_PER
+#define GP_SHARD_PER 4
+#endif
+constexpr uint32_t kShardPer = GP_SHARD_PER;
 
 // Sharded push-sum link pass: a link message whose CSR slot is this rank's gets the slot's round tag
 // (the receiver reads msg_prev[u] itself, as on one GPU); one whose slot belongs to another rank goes
@@ -1275,7 +1314,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_link_scatter_x(RoundArgs a, Xchg 
     block_reserve(x, rm, q, pos);
 #pragma unroll
     for (uint32_t j = 0; j < kShardPer; ++j)
-        if (rm[j]) put<true>(x, q[j], pos[j], lp[j], mm[j]);
+        if (rm[j]) put_t<true>(x, q[j], pos[j], lp[j], mm[j]);
 }
 
 __global__ __launch_bounds__(kBlock) void k_gs_link_scatter_x(RoundArgs a, Xchg x) {
@@ -1303,7 +1342,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_link_scatter_x(RoundArgs a, Xchg 
     block_reserve(x, rm, q, pos);
 #pragma unroll
     for (uint32_t j = 0; j < kShardPer; ++j)
-        if (rm[j]) put<false>(x, q[j], pos[j], lp[j] | ((nl[j] - 1u) << 31), make_double2(0.0, 0.0));
+        if (rm[j]) put_t<false>(x, q[j], pos[j], lp[j] | ((nl[j] - 1u) << 31), make_double2(0.0, 0.0));
 }
 
 // Halo faces of F(k), after the round kernel: the direction bytes of this rank's first plane go
@@ -1715,7 +1754,7 @@ __device__ __forceinline__ void gs_push_body(const RoundArgs& a, const Xchg* xp)
             block_reserve(x, remote, q, pos);
 #pragma unroll
             for (uint32_t c = 0; c < 2; ++c)
-                if (remote[c]) put<false>(x, q[c], pos[c], t[c], make_double2(0.0, 0.0));
+                if (remote[c]) put_t<false>(x, q[c], pos[c], t[c], make_double2(0.0, 0.0));
         }
     }
     if (r) block_add(newly, a.parts, (long long)r - 1);
@@ -2379,7 +2418,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_full4x(RoundArgs a, Xchg x) {
             block_reserve(x, want, peer, pos, sub);
 #pragma unroll
             for (uint32_t k = 0; k < 8; ++k)
-                if (want[k]) put<false>(x, peer[k], pos[k], tgt[k], make_double2(0.0, 0.0), sub);
+                if (want[k]) put_t<false>(x, peer[k], pos[k], tgt[k], make_double2(0.0, 0.0), sub);
         }
         // the reports of this round into the done bitmap: 8 lanes = 32 actors = one word
         uint32_t w = done4 << ((q & 7u) * 4u);
@@ -2615,6 +2654,7 @@ static_assert(kMaxWorld * kSub == kBlock, "block_reserve_qs: one LDS counter per
 __device__ __forceinline__ uint32_t block_reserve_qs(const Xchg& x, bool want, uint32_t q, uint32_t sb) {
     __shared__ uint32_t cnt[kMaxWorld * kSub], base[kMaxWorld * kSub];
     cnt[threadIdx.x] = 0u;
+    peer_tab_fill(x);
     __syncthreads();
     const uint32_t key = q * kSub + sb;
     const uint32_t pos = want ? atomicAdd(&cnt[key], 1u) : 0u;
@@ -2718,7 +2758,7 @@ __global__ __launch_bounds__(kBlock) void k_gs_sparse_x(RoundArgs a, Xchg x, GsS
         if (__syncthreads_or(remote)) {  // block-uniform
             const uint32_t sb = (v >> 10) % kSub;
             const uint32_t pos = block_reserve_qs(x, remote, q, sb);
-            if (remote) put<false>(x, q, pos, u0, make_double2(0.0, 0.0), sb);
+            if (remote) put_t<false>(x, q, pos, u0, make_double2(0.0, 0.0), sb);
         }
     }
     if (r) block_add(newly, a.parts, (long long)r - 1);
