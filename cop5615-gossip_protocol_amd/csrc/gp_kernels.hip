@@ -1271,7 +1271,7 @@ __device__ __forceinline__ void block_reserve(const Xchg& x, const bool (&want)[
 // Actors per thread of the sharded link passes (block-strided): more per block means fewer
 // block-level reservations (three barriers and one global atomic per peer each).
 #ifndef GP_SHARD_PER
-#define GP_SHARD_PER 4
+#define GP_SHARD_PER 4  // (C5 / 8 link scatter: 4 0.61 ms, 8 0.63, 16 0.96; profiles/round6/put_ab/)
 #endif
 constexpr uint32_t kShardPer = GP_SHARD_PER;
 
