@@ -46,6 +46,9 @@ constexpr size_t kTallyThrDiv = GP_TALLY_THR_DIV;
 #ifndef GP_SHARD_BINS
 #define GP_SHARD_BINS 1  // A/B knob: full gossip shards' receipt wave in bins (k_gs_bins_*)
 #endif
+#ifndef GP_BIN_GRID
+#define GP_BIN_GRID 1024  // workgroups of the bins' count and placement passes (A/B knob)
+#endif
 #ifndef GP_BIN_DIV
 #define GP_BIN_DIV 16    // a round runs in bins when its receipts (estimated, every rank's) are >= actors / this
 #endif
@@ -911,8 +914,10 @@ int launch_aux(Handle* h, int64_t k, const Xchg* x, int piece = 0) {
             if (x) launch_gs_link_scatter_x(a, *x, l);
             else launch_link_count(a, l);
         }
-        // (a list round's last block ran it: k_gs_sparse_x)
-        if (h->generic && x && h->world > 1 && h->sp_fused != k) launch_shard_done_out(a, *x, h->stream);
+        // (a list round's last block ran it: k_gs_sparse_x; a round in bins sends no done words: the peers'
+        // replicas only feed the sender-side filter, which those rounds do not run, and a word left
+        // unshipped goes out with a later round's, as any word past a plan's capacity does)
+        if (h->generic && x && h->world > 1 && h->sp_fused != k && !x->binned) launch_shard_done_out(a, *x, h->stream);
     } else if (h->generic) {
         const int c = (int)(r & 1u);
         launch_exclusive_scan(h->bcnt[c], h->boff[c], h->g.actors, h->scan_scratch, h->stream);
@@ -2152,16 +2157,17 @@ int create(const gp_config* cfg, int32_t rank, int32_t world, bool sharded, gp_l
                 uint32_t nbt = 0;
                 for (int q = 0; q < h->world; ++q) {
                     b.bin0[q] = nbt;
-                    if (q != h->rank) nbt += bins_of(h, q);
+                    nbt += bins_of(h, q);
                 }
                 b.bin0[h->world] = nbt;
                 b.nbt = nbt;
                 b.nb_self = bins_of(h, h->rank);
-                b.W = (uint32_t)std::min(grid_for((uint32_t)n), 1024);
+                b.W = (uint32_t)std::min(grid_for((uint32_t)n), GP_BIN_GRID);
                 const size_t nc = (size_t)nbt * b.W;
+                b.self_words = b.nb_self + 1u + (uint32_t)((n + 1) / 2) + 1u;  // one u16 receipt per own actor
                 if (nbt && nbt <= kMaxBins && nc < (1u << 31)) {
                     if ((rc = h->alloc(&b.cnt, nc)) || (rc = h->alloc(&b.off, nc + 1)) ||
-                        (rc = h->alloc(&b.scratch, scan_scratch_words((uint32_t)nc))))
+                        (rc = h->alloc(&b.scratch, scan_scratch_words((uint32_t)nc))) || (rc = h->alloc(&b.self, b.self_words)))
                         return bail(rc);
                 }
             }

@@ -344,17 +344,20 @@ int prepare_gs_tally();  // once per process: allow the tally pass's 128 KB of d
 // (k_gs_bins_count) counts them per (peer, bin) and workgroup in LDS, an exclusive scan gives every
 // (peer, bin, workgroup) its place, and k_gs_bins_place draws the same receipts again into their places,
 // as u16 offsets in the bin.  The chunk's entry part then holds the bins' starts (nb + 1 u32 words,
-// nb = the receiver's bins) and the u16 entries.  The receiver counts a bin per workgroup in LDS and
-// adds the counts to its receipt words (k_shard_unpack_bins): no fabric atomics, 2 bytes a receipt.
+// nb = the receiver's bins) and the u16 entries.  The rank's own receipts take the same way into a
+// chunk of its own (`self`), so the receiver counts every receipt of a bin per workgroup in LDS and
+// writes its receipt words whole (k_shard_unpack_bins): no fabric atomics anywhere, 2 bytes a receipt.
 // No sender-side done filter in these rounds: F(k + 1) drops the receipts of done actors itself.
 struct GsBins {
-    uint32_t* cnt;                 // [nbt][W]: receipts per (peer, bin) and workgroup (tally_col order)
+    uint32_t* cnt;                 // [nbt][W]: receipts per (rank, bin) and workgroup (tally_col order)
     uint32_t* off;                 // its exclusive scan, nbt * W + 1 words
     uint32_t* scratch;             // the scan's scratch
+    uint32_t* self;                // the own receipts' chunk: nb_self + 1 starts, then u16 entries
+    uint32_t self_words;           // its size (room for one receipt per own actor: "full" holds one chain)
     uint32_t W;                    // grid of k_gs_bins_count / k_gs_bins_place (a multiple of 8)
-    uint32_t nbt;                  // bins over every peer
+    uint32_t nbt;                  // bins over every rank (this one's too)
     uint32_t nb_self;              // bins of this rank's range (the receiver's grid)
-    uint32_t bin0[kMaxWorld + 1];  // first bin of each peer (this rank: none), bin0[world] = nbt
+    uint32_t bin0[kMaxWorld + 1];  // first bin of each rank, bin0[world] = nbt
 };
 constexpr uint32_t kMaxBins = 8192;  // the passes' LDS counters (u32 per bin)
 int prepare_gs_bins();               // once per process: the receiver's 128 KB of dynamic LDS (0: ok)

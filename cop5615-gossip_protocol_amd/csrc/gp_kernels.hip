@@ -2463,9 +2463,10 @@ __device__ __forceinline__ uint32_t bins_room(uint32_t cap, uint32_t nb) {
     return w > nb + 1u ? 2u * (w - nb - 1u) : 0u;
 }
 
-// F(r) of a receipt-wave round: k_gs_full4x's walk, apply and draws; a local receipt is an atomic as
-// there, a remote one is counted in its (peer, bin) LDS counter, written out per workgroup for the scan.
-// Every receipt is sent (no sender-side filter: a bin entry costs less than the filter's bitmap read).
+// F(r) of a receipt-wave round: k_gs_full4x's walk, apply and draws; every receipt is counted in its
+// (rank, bin) LDS counter, written out per workgroup for the scan (a local receipt too: the memory-side
+// atomic it took cost ~80 us of this kernel's ~160 per rank-round at C4 / 8).  Every receipt is sent
+// (no sender-side filter: a bin entry costs less than the filter's bitmap read).
 __global__ __launch_bounds__(kBlock) void k_gs_bins_count(RoundArgs a, Xchg x, GsBins b) {
     extern __shared__ uint32_t lc[];
     const uint32_t r = a.r;
@@ -2509,13 +2510,9 @@ __global__ __launch_bounds__(kBlock) void k_gs_bins_count(RoundArgs a, Xchg x, G
 #pragma unroll
                 for (uint32_t c = 0; c < 2; ++c) {
                     if (tok <= c) break;
-                    if (u[c] - lo < hi - lo) {
-                        atomicAdd(&a.inc_cur[u[c]], 1u);
-                    } else {
-                        uint32_t qq, bin;
-                        peer_bin(x, b, u[c], qq, bin);
-                        atomicAdd(&lc[bin], 1u);
-                    }
+                    uint32_t qq, bin;  // (this rank's own actors too: its own chunk)
+                    peer_bin(x, b, u[c], qq, bin);
+                    atomicAdd(&lc[bin], 1u);
                 }
             }
         }
@@ -2559,17 +2556,28 @@ __global__ __launch_bounds__(kBlock) void k_gs_bins_place(RoundArgs a, Xchg x, G
     const bool live = !(r && prev >= a.target);
     const uint32_t col = tally_col(blockIdx.x, b.W);
     for (uint32_t i = threadIdx.x; i < b.nbt; i += kBlock) lp[i] = b.off[i * b.W + col];
-    if (threadIdx.x < x.world) {  // per peer: first entry, room, first actor, entries (LDS: per-lane reads)
+    // per rank: first entry, room, first actor, entries (LDS: per-lane reads).  (A per-lane index into
+    // the kernel arguments, or a pointer chosen between two of them, makes the compiler copy all 1.8 KB
+    // of them to every thread's scratch: 0.5 GB of writes per launch at C4 / 8.)
+    if (threadIdx.x < x.world) {
         const uint32_t qq = threadIdx.x, nb = b.bin0[qq + 1u] - b.bin0[qq];
         pbase[qq] = b.off[b.bin0[qq] * b.W];
-        proom[qq] = qq == x.rank ? 0u : bins_room(x.out[qq].cap, nb);
         pabnd[qq] = x.abnd[qq];
-        pe16[qq] = qq == x.rank ? nullptr : reinterpret_cast<uint16_t*>(x.out[qq].slot + nb + 1u);
+        if (qq != x.rank) {
+            proom[qq] = bins_room(x.out[qq].cap, nb);
+            pe16[qq] = reinterpret_cast<uint16_t*>(x.out[qq].slot + nb + 1u);
+        }
+    }
+    const uint32_t nbs = b.bin0[x.rank + 1u] - b.bin0[x.rank];  // this rank's own chunk
+    if (threadIdx.x == 0) {
+        proom[x.rank] = 2u * (b.self_words - nbs - 1u);
+        pe16[x.rank] = reinterpret_cast<uint16_t*>(b.self + nbs + 1u);
     }
     __syncthreads();
-    if (blockIdx.x == 0) {  // the bin starts, relative to each peer's first entry
+    if (blockIdx.x == 0) {  // the bin starts, relative to each rank's first entry
+        for (uint32_t i = threadIdx.x; i <= nbs; i += kBlock) b.self[i] = b.off[(b.bin0[x.rank] + i) * b.W] - pbase[x.rank];
         for (uint32_t qq = 0; qq < x.world; ++qq) {
-            if (qq == x.rank) continue;
+            if (qq == x.rank) continue;  // (its own chunk holds every own receipt: no overflow, no header)
             const uint32_t nb = b.bin0[qq + 1u] - b.bin0[qq];
             for (uint32_t i = threadIdx.x; i <= nb; i += kBlock) x.out[qq].slot[i] = b.off[(b.bin0[qq] + i) * b.W] - pbase[qq];
             if (threadIdx.x < kSub) {
@@ -2604,7 +2612,6 @@ __global__ __launch_bounds__(kBlock) void k_gs_bins_place(RoundArgs a, Xchg x, G
 #pragma unroll
             for (uint32_t c = 0; c < 2; ++c) {
                 if (tok <= c) break;
-                if (u[c] - lo < hi - lo) continue;  // local: added by F(r)
                 uint32_t qq, bin;
                 peer_bin(x, b, u[c], qq, bin);
                 const uint32_t pos = atomicAdd(&lp[bin], 1u) - pbase[qq];
@@ -2614,9 +2621,10 @@ __global__ __launch_bounds__(kBlock) void k_gs_bins_place(RoundArgs a, Xchg x, G
     }
 }
 
-// The receiver of a receipt-wave round: workgroup = one bin of this rank's actors; every peer's entries
-// of the bin counted in LDS, then added to the receipt words (local receipts are already there).  A
-// done actor's receipts are added too: F(r + 1) ignores them (program.fs:92's filter, at the receiver).
+// The receiver of a receipt-wave round: workgroup = one bin of this rank's actors; every rank's entries
+// of the bin (its own from its own chunk) counted in LDS, then written as the bin's receipt words, zeros
+// included.  A done actor's receipts are counted too: F(r + 1) ignores them (program.fs:92's filter, at
+// the receiver).
 constexpr uint32_t kBinBlock = 1024;
 __global__ __launch_bounds__(kBinBlock) void k_shard_unpack_bins(RoundArgs a, Xchg x, GsBins b) {
     extern __shared__ uint32_t h[];
@@ -2627,15 +2635,17 @@ __global__ __launch_bounds__(kBinBlock) void k_shard_unpack_bins(RoundArgs a, Xc
     const uint32_t base = x.abnd[x.rank] + (bin << kTallyShift), top = x.abnd[x.rank + 1u];
     const uint32_t n = top - base < S ? top - base : S;
     for (uint32_t qq = 0; qq < x.world; ++qq) {
+        const bool own = qq == x.rank;
         const PeerIn& in = x.in[qq];
-        if (qq == x.rank || !in.cap || !in.hdr->binned) continue;  // uniform
-        const uint32_t room = bins_room(in.cap, nb), e = in.slot[nb];
-        const uint32_t s0 = in.slot[bin], s1 = min(in.slot[bin + 1u], min(e, room));
+        if (!own && (!in.cap || !in.hdr->binned)) continue;  // uniform
+        const uint32_t* tab = own ? b.self : in.slot;
+        const uint32_t room = own ? 2u * (b.self_words - nb - 1u) : bins_room(in.cap, nb), e = tab[nb];
+        const uint32_t s0 = tab[bin], s1 = min(tab[bin + 1u], min(e, room));
         if (s0 > s1) {  // a corrupt chunk: reported, never applied
-            if (threadIdx.x == 0 && s0 > in.slot[bin + 1u]) atomicOr(x.overflow, 2u);
+            if (threadIdx.x == 0 && s0 > tab[bin + 1u]) atomicOr(x.overflow, 2u);
             continue;
         }
-        const uint16_t* e16 = reinterpret_cast<const uint16_t*>(in.slot + nb + 1u);
+        const uint16_t* e16 = reinterpret_cast<const uint16_t*>(tab + nb + 1u);
         for (uint32_t i = s0 + threadIdx.x; i < s1; i += kBinBlock) {
             const uint32_t t = e16[i];
             if (t < n) atomicAdd(&h[t], 1u);
@@ -2643,8 +2653,7 @@ __global__ __launch_bounds__(kBinBlock) void k_shard_unpack_bins(RoundArgs a, Xc
         }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += kBinBlock)
-        if (const uint32_t c = h[i]) a.inc_cur[base + i] += c;
+    for (uint32_t i = threadIdx.x; i < n; i += kBinBlock) a.inc_cur[base + i] = h[i];
 }
 
 // Positions of one entry per thread in peer q's chunk, sub-segment sb (both per thread): LDS counters

@@ -169,3 +169,25 @@ def test_flag_values_match_header():
     assert flags, "no GP_FLAG_* in the header"
     for name, value in flags.items():
         assert getattr(_abi, "FLAG_" + name) == value, name
+
+
+def test_kernels_use_no_scratch(tmp_path):
+    """Every gfx950 kernel of the built library keeps its state in registers and LDS: no private
+    (scratch) segment and no spilled VGPRs.  (A per-lane index into the kernel arguments once made the
+    compiler copy all of them to every thread's scratch: 0.5 GB of writes per launch at C4 / 8.)"""
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(f"{llvm}/clang-offload-bundler"):
+        pytest.skip("no ROCm LLVM tools")
+    fat, co = tmp_path / "fatbin.bin", tmp_path / "gfx950.co"
+    subprocess.run([f"{llvm}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", _abi.LIB_PATH], check=True)
+    subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    notes = subprocess.run([f"{llvm}/llvm-readelf", "--notes", str(co)], check=True, capture_output=True,
+                           text=True).stdout
+    names = re.findall(r"^\s*\.name:\s+(\S+)", notes, re.M)
+    kernels = [n for n in names if n.startswith("_Z")]
+    private = [int(x) for x in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)]
+    spills = [int(x) for x in re.findall(r"\.vgpr_spill_count:\s+(\d+)", notes)]
+    assert len(kernels) >= 40 and len(private) == len(kernels) == len(spills), (len(kernels), len(private))
+    bad = [(k, p, v) for k, p, v in zip(kernels, private, spills) if p or v]
+    assert not bad, bad
