@@ -50,7 +50,10 @@ constexpr size_t kTallyThrDiv = GP_TALLY_THR_DIV;
 #define GP_BIN_GRID 1024  // workgroups of the bins' count and placement passes (A/B knob)
 #endif
 #ifndef GP_BIN_DIV
-#define GP_BIN_DIV 16    // a round runs in bins when its receipts (estimated, every rank's) are >= actors / this
+// a round runs in bins while its receipts (estimated, every rank's) are >= actors / this (C4 / 8 rank
+// kernels per run, incl. the loopback copies: 2 13.14 ms, 4 13.25, 8 13.29, 16 13.31;
+// profiles/round6/bins_div_ab.txt)
+#define GP_BIN_DIV 2
 #endif
 #ifndef GP_SHARD_RAMP
 #define GP_SHARD_RAMP 1  // A/B knob: the same on shards (k_gs_sparse_x)
@@ -914,10 +917,13 @@ int launch_aux(Handle* h, int64_t k, const Xchg* x, int piece = 0) {
             if (x) launch_gs_link_scatter_x(a, *x, l);
             else launch_link_count(a, l);
         }
-        // (a list round's last block ran it: k_gs_sparse_x; a round in bins sends no done words: the peers'
-        // replicas only feed the sender-side filter, which those rounds do not run, and a word left
-        // unshipped goes out with a later round's, as any word past a plan's capacity does)
-        if (h->generic && x && h->world > 1 && h->sp_fused != k && !x->binned) launch_shard_done_out(a, *x, h->stream);
+        // (a list round's last block ran it: k_gs_sparse_x.  A round in bins sends no done words while a
+        // quarter of the nodes or more have not reported: the peers' replicas only feed the sender-side
+        // filter, which those rounds do not run, and a word left unshipped goes out with a later round's,
+        // as any word past a plan's capacity does; the last rounds of the wave ship them, so the filter
+        // of the rounds after it starts current)
+        const bool skip_done = x && x->binned && (h->lay.nodes - h->completed) * 4 > h->lay.nodes;
+        if (h->generic && x && h->world > 1 && h->sp_fused != k && !skip_done) launch_shard_done_out(a, *x, h->stream);
     } else if (h->generic) {
         const int c = (int)(r & 1u);
         launch_exclusive_scan(h->bcnt[c], h->boff[c], h->g.actors, h->scan_scratch, h->stream);
