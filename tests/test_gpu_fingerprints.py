@@ -73,6 +73,10 @@ def test_shards_vs_fingerprint(name, world):
         assert (int(st.round), int(st.completed)) == (fp["rounds"], fp["completed"])
         np.testing.assert_array_equal(e.read_trace(), unpack_trace(fp["trace_z"]))
     _check(fp, sts[0], engines[0].read_trace(), _shard_arrays(engines, fp["algorithm"]))
+    if fp["algorithm"] == "gossip":  # C4 x 8 runs all three kinds of rounds: lists, bins, entries (§6.6)
+        ss = engines[0].shard_stats()
+        assert ss["list_rounds"] > 0 and ss["bin_rounds"] > 0, ss
+        assert ss["list_rounds"] + ss["bin_rounds"] + 1 < fp["rounds"], ss
     for e in engines:
         e.close()
 

@@ -381,9 +381,10 @@ def test_full_gossip_shard_bins_vs_oracle(n, world, seed, tiers):
 
 def test_full_gossip_shard_bins_default_wave():
     """Without the test hook the receipt wave runs in bins (the chain bound times the share of nodes not
-    done at least actors / 16), the ramp on lists before it and entries with the sender filter after it:
-    all three kinds of rounds in one run at 2M actors on 8 ranks, bit-exact against the single-GPU engine."""
-    n, world, seed = 2_000_000, 8, 3
+    done at least actors / GP_BIN_DIV), the ramp on lists before it and entries with the sender filter
+    after it: all three kinds of rounds in one run at 16M actors on 8 ranks, bit-exact against the
+    single-GPU engine (the C4 x 8 fingerprint test checks the same at 100M)."""
+    n, world, seed = 16_000_000, 8, 3
     ref = Simulator(n, "full", "gossip", seed=seed)
     rs = ref.step()
     engines = _shards(n, "full", "gossip", world, seed)
