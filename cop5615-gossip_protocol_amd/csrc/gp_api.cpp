@@ -2566,7 +2566,10 @@ int group_create(const gp_config* cfg, gp_layout* out, void** handle) {
         c.device = G.dev[p];
         c.num_gpus = 0;
         c.flags &= ~(GP_FLAG_ONE_DEVICE | GP_FLAG_GROUP | GP_FLAG_USE_STREAM);
-        c.flags |= GP_FLAG_PIECES;  // the group exchanges piece by piece (its own transport)
+        // the group exchanges piece by piece (its own transport): always on one device (device copies on
+        // a side stream, in the GPU suite); across devices only when the caller asks (GP_FLAG_PIECES): its
+        // RCCL path on per-shard side streams has not run on two devices yet
+        if (G.one_device) c.flags |= GP_FLAG_PIECES;
         c.stream = nullptr;
         if (G.one_device) {
             c.flags |= GP_FLAG_USE_STREAM;

@@ -218,6 +218,24 @@ __device__ __forceinline__ void peer_tab_fill(const Xchg& x) {
         t.cap[threadIdx.x] = o.cap;
     }
 }
+// The two halo faces' entry parts, likewise (a shard's tail round writes them itself).
+struct HaloTab {
+    uint32_t* slot[2];
+    double2* msg[2];
+    uint32_t cap[2];
+};
+__device__ __forceinline__ HaloTab& halo_tab() {
+    __shared__ HaloTab t;
+    return t;
+}
+__device__ __forceinline__ void halo_tab_fill(const Xchg& x) {
+    if (threadIdx.x < 2u) {
+        HaloTab& t = halo_tab();
+        t.slot[threadIdx.x] = x.h.out_slot[threadIdx.x];
+        t.msg[threadIdx.x] = x.h.out_msg[threadIdx.x];
+        t.cap[threadIdx.x] = x.h.out_cap[threadIdx.x];
+    }
+}
 template <bool MSG>
 __device__ __forceinline__ void put_t(const Xchg& x, uint32_t q, uint32_t pos, uint32_t entry, double2 m,
                                       uint32_t sub = kSub) {
@@ -824,6 +842,15 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
     const uint8_t tag = (uint8_t)a.tag_cur;  // link_tag(r)
     if constexpr (Q) {
         const bool tail = skip;  // block-uniform: the compacted segment walk of the run's tail
+        if constexpr (LM == 2) {
+            // a tail round's entries read the peers' chunks and the halo faces from LDS (put_t): a
+            // lane's own peer or face indexing the kernel arguments is a vector load per field
+            if (tail) {
+                peer_tab_fill(*xp);
+                halo_tab_fill(*xp);
+                __syncthreads();
+            }
+        }
         TailWalk t = tail_walk(a, tail);
         uint32_t walked = 0;
         for (;;) {
@@ -871,12 +898,13 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
                         if (cross) q = x.world + sd;
                     }
                     const uint32_t pos = wave_reserve(x, remote || cross, q);
-                    if (remote) put<true>(x, q, pos, lp, ls.msg);
+                    if (remote) put_t<true>(x, q, pos, lp, ls.msg);
                     if (cross) {
-                        const uint32_t cap = x.h.out_cap[sd];
+                        const HaloTab& ht = halo_tab();
+                        const uint32_t cap = ht.cap[sd];
                         if (pos < cap) {
-                            x.h.out_slot[sd][my_sub() * cap + pos] = fo;
-                            x.h.out_msg[sd][my_sub() * cap + pos] = ls.msg;
+                            ht.slot[sd][my_sub() * cap + pos] = fo;
+                            ht.msg[sd][my_sub() * cap + pos] = ls.msg;
                         } else {
                             atomicOr(x.overflow, 1u);
                         }

@@ -32,14 +32,16 @@ class Simulator:
                  kernel_timing: bool = False, generic: bool = False, stream: int | None = None,
                  num_gpus: int = 1, one_device: bool = False, group: bool = False, quiet_waves: bool = False,
                  gossip_tally: bool = False, full_plan: bool = False, tight_tiers: bool = False,
-                 tally_fallbacks: bool = False, force_pieces: bool = False, one_round: bool = False):
+                 tally_fallbacks: bool = False, force_pieces: bool = False, one_round: bool = False,
+                 pieces: bool = False):
         """num_gpus > 1: one graph over devices device .. device+num_gpus-1 of this process (the
         library's own RCCL exchange); one_device: all of them on `device` (device-copy exchange);
         group: the multi-GPU engine also for num_gpus = 1; quiet_waves: quiet-wave skipping at any
         graph size (a test hook; it is on by default from 2^20 actors); tally_fallbacks: the receipt
         tally's counted-batch placement and 32-bit receipt escape everywhere (a test hook);
         force_pieces: num_gpus > 1, rounds in 4 pieces at any size (a test hook; the group runs
-        them from 2^25 actors per shard)."""
+        them from 2^25 actors per shard); pieces: num_gpus > 1 across devices, exchange in pieces too
+        (on by itself with one_device; across devices opt-in until its RCCL path has run on two)."""
         if topology not in _abi.TOPOLOGIES:
             raise ValueError(f"unknown topology {topology!r} (case-sensitive: {list(_abi.TOPOLOGIES)})")
         if algorithm not in _abi.ALGOS:
@@ -51,6 +53,7 @@ class Simulator:
         flags |= _abi.FLAG_GOSSIP_TALLY if gossip_tally else 0
         flags |= _abi.FLAG_TALLY_FALLBACKS if tally_fallbacks else 0
         flags |= _abi.FLAG_FORCE_PIECES if force_pieces else 0
+        flags |= _abi.FLAG_PIECES if pieces or force_pieces else 0
         flags |= _abi.FLAG_ONE_ROUND if one_round else 0
         # num_gpus > 1: the exchange plan of the shards (activity tiers; see sharded.HipShard)
         flags |= (_abi.FLAG_FULL_PLAN if full_plan else 0) | (_abi.FLAG_TIGHT_TIERS if tight_tiers else 0)

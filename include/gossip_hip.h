@@ -73,7 +73,9 @@ enum gp_flags {
                                   one piece overlaps the next piece's kernels; the library runs 4
                                   pieces when every rank holds 2^25 actors or more, until half the
                                   nodes have converged, else 1 (gp_shard_pieces, re-read after
-                                  every gp_shard_sync) */
+                                  every gp_shard_sync).  The library's own group
+                                  (num_gpus > 1) runs pieces always under GP_FLAG_ONE_DEVICE and
+                                  across devices only with this flag (ABI 8) */
     GP_FLAG_FORCE_PIECES = 2048, /* with GP_FLAG_PIECES: 4 pieces at any size (whole z-planes, or
                                   256 actors on line / 2D, permitting); a test hook, same results */
     GP_FLAG_ONE_ROUND = 4096,    /* one GPU: one round per launch, also where the library batches
