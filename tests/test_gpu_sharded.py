@@ -535,6 +535,45 @@ def test_shards_random_sweep(n, topo, algo, seed, world):
         e.close()
 
 
+def _full_gossip_sweep(count=24, seed=2026):
+    """Seeded random full-gossip shard jobs: sizes log-uniform over 64..1.5M, 2..8 ranks, one of the
+    plans and the bins' test hook drawn per case."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(count):
+        n = int(np.exp(rng.uniform(np.log(64), np.log(1_500_000))))
+        out.append((n, int(rng.integers(1, 1 << 30)), int(rng.integers(2, 9)),
+                    ("default", "tight", "full")[rng.integers(3)], bool(rng.integers(2))))
+    return out
+
+
+@pytest.mark.parametrize("n,seed,world,plan,bins", _full_gossip_sweep())
+def test_full_gossip_shards_random_sweep(n, seed, world, plan, bins):
+    """Full gossip on shards over random jobs, every kind of round the engine has (the ramp on lists, the
+    receipt wave in bins — forced in every round past the lists when `bins` — and entries with the
+    sender filter) under a random plan, bit-exact against the oracle to convergence."""
+    try:
+        sharded.partition(n, "full", world)
+    except GossipError as e:
+        if "cannot be split" not in str(e):
+            raise
+        pytest.skip(str(e))
+    kw = {"tight_tiers": True} if plan == "tight" else {"full_plan": True} if plan == "full" else {}
+    ref = oracle.OracleSim(n, "full", "gossip", seed=seed)
+    rs = ref.step(threads=8)
+    engines = _shards(n, "full", "gossip", world, seed, force_bins=bins, **kw)
+    sts = sharded.run_local(engines)
+    for st in sts:
+        assert (st.round, st.completed, st.converged) == (rs.round, rs.completed, rs.converged)
+    _check_vs(ref, engines, "gossip")
+    ss = engines[0].shard_stats()
+    assert ss["list_rounds"] > 0, ss
+    if bins:
+        assert ss["bin_rounds"] > 0, ss
+    for e in engines:
+        e.close()
+
+
 def test_shard_tables_scale_with_rank_count():
     """Per-rank link tables: a rank holds the CSR of its own receivers and the
     `lpos` of its own senders, not the global tables, so its device memory is its share of the
