@@ -230,6 +230,7 @@ struct Handle {
     int64_t plan_changes = 0, restores = 0;
     uint32_t* pcount = nullptr;
     uint32_t* overflow = nullptr;
+    uint32_t* xfin = nullptr;      // push-sum tail rounds: k_ps_quiet_x<true>'s finished workgroups (Xchg::fin)
     unsigned long long* self_newly = nullptr;
     void* pending_send = nullptr;  // gp_shard_round issued, gp_shard_deliver not yet
     bool awaiting_deliver = false;
@@ -1342,8 +1343,10 @@ int build_plan(Handle* h) {
         return fail(GP_ENOMEM, "a receive buffer of %lld bytes is past the slot references' reach", (long long)rt);
     int rc;
     if ((rc = h->alloc(&h->pcount, ((size_t)W + 2) * kSub * kCtrStride)) || (rc = h->alloc(&h->overflow, 1)) ||
-        (rc = h->alloc(&h->self_newly, 1)) || (rc = h->alloc(&h->pmax, (size_t)kMaxPieces * kMaxWorld)))
+        (rc = h->alloc(&h->self_newly, 1)) || (rc = h->alloc(&h->pmax, (size_t)kMaxPieces * kMaxWorld)) ||
+        (rc = h->alloc(&h->xfin, (size_t)(kFinGroups + 1) * kFinStride)))
         return rc;
+    HIP_TRY(hipMemsetAsync(h->xfin, 0, (size_t)(kFinGroups + 1) * kFinStride * sizeof(uint32_t), h->stream));
     return GP_OK;
 }
 
@@ -1366,6 +1369,7 @@ Xchg base_xchg(const Handle* h) {
     x.dship = h->dship;
     x.dstat = h->dstat;
     x.binned = h->bin_next ? 1u : 0u;
+    x.fin = h->xfin;
     return x;
 }
 
@@ -1469,7 +1473,8 @@ int shard_round_piece(Handle* h, void* send, int piece) {
     // the halo face this piece holds (the rank's first actors to rank-1, its last to rank+1), then the
     // headers
     if (!x.hin) launch_shard_halo(a, x, h->gossip ? 0 : 1, h->stream);
-    if (h->sp_fused != k) launch_shard_pack(a, x, applied_round(h, k), h->stream);  // (a list round packed itself)
+    // (a full-gossip list round and a push-sum tail round with the halo faces inline packed themselves)
+    if (h->sp_fused != k && !x.hin) launch_shard_pack(a, x, applied_round(h, k), h->stream);
     HIP_TRY(hipGetLastError());
     for (int q = 0; q < h->world; ++q) h->bytes_sent += (int64_t)h->out_chunk[(size_t)piece * h->world + q].size;
     if (++h->piece_next == h->npiece) {

@@ -227,6 +227,9 @@ struct Xchg {
     uint32_t* dship;                  // own done words as last shipped (global word index)
     uint32_t* dstat;                  // [kDstatWords]: dirty-word counter, backlog flag
     uint32_t binned;                  // full gossip: this round's receipts travel in bins (GsBins)
+    uint32_t* fin;                    // push-sum, tail rounds: workgroups of k_ps_quiet_x<true> finished, per
+                                      // group ([1 + g] * kFinStride) and groups finished ([0]); the last one
+                                      // packs the headers (0 between launches)
     PeerOut out[kMaxWorld];
     PeerIn in[kMaxWorld];
     HaloX h;
@@ -331,6 +334,9 @@ struct GsSparse {
                       // and the pack; 0 between launches)
 };
 constexpr uint32_t kSpStride = 32, kSpSlack = 1024;
+// A push-sum shard's tail round counts its finished workgroups in kFinGroups groups (one counter per
+// 128-byte line) before one counter of groups (Xchg::fin).
+constexpr uint32_t kFinGroups = 32, kFinStride = 32;
 void launch_gs_sparse(const RoundArgs& a, const GsTally& t, const GsSparse& sp, const Launch& l);
 // shards: F(k) on lists, then (its last block) k_shard_done_out's and k_shard_pack's work for round k
 void launch_gs_sparse_x(const RoundArgs& a, const Xchg& x, const GsSparse& sp, long long applied, const Launch& l);

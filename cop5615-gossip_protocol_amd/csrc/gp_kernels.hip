@@ -805,6 +805,33 @@ __device__ __forceinline__ bool tail_next(const RoundArgs& a, TailWalk& t, uint8
 // HIN (LM 2, tail rounds only: the host knows from the synced count): the walk writes the halo faces
 // itself, the direction byte of every face actor and the messages that cross, so k_shard_halo is not
 // launched.
+__device__ __forceinline__ void shard_pack_body(const RoundArgs& a, const Xchg& x, long long applied);
+// A shard's tail round (k_ps_quiet_x<true>): the workgroup that finishes last packs the round's headers
+// (k_shard_pack's work) — every workgroup's counts and entries are released before its arrival is
+// counted and acquired by the last one — so the round is one launch fewer.  Every thread calls it.
+__device__ __forceinline__ void tail_pack(const RoundArgs& a, const Xchg& x) {
+    __shared__ uint32_t last_s;
+    // What the pack reads was written with device-scope atomics (the entry and halo counters, the round's
+    // sub-counters, the overflow flag); a wave's atomics have been performed once its memory counter is 0,
+    // so a workgroup arrives without a device-scope release (an L2 write-back per workgroup: ~1800 of
+    // them made the tail round 94.5 -> 155.8 us).  The arrivals go to kFinGroups counters (one XCD's
+    // workgroups each), the last of each group to one counter of groups.
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t G = gridDim.x < kFinGroups ? gridDim.x : kFinGroups, g = blockIdx.x % G;
+        const uint32_t in_g = (gridDim.x - g + G - 1u) / G;  // workgroups of group g
+        uint32_t last = 0u;
+        if (atomicAdd(x.fin + (1u + g) * kFinStride, 1u) == in_g - 1u) last = atomicAdd(x.fin, 1u) == G - 1u;
+        last_s = last;
+    }
+    __syncthreads();
+    if (!last_s) return;
+    __threadfence();
+    shard_pack_body(a, x, (long long)a.r);
+    if (threadIdx.x <= kFinGroups) x.fin[threadIdx.x * kFinStride] = 0u;  // the next tail round counts from 0
+}
+
 template <int LM, bool Q, bool HIN = false>
 __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp = nullptr) {
     const Geom g = a.g;
@@ -836,7 +863,10 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
     }
     // converged after round r - 1 (one GPU, small graphs: Q = false, the per-wave gate)
     const unsigned long long prev = (Q || LM == 2) ? gate_count(a, a.r) : gate_count_wave(a, a.r);
-    if (prev >= a.target) return;
+    if (prev >= a.target) {  // (block-uniform; a tail round's headers still go out)
+        if constexpr (LM == 2 && HIN) tail_pack(a, *xp);
+        return;
+    }
     const bool mark = Q && prev >= a.act_thr;                          // F(r) marks round r + 1
     const bool skip = Q && r >= 2u && a.total[r - 2] >= a.act_thr;  // F(r - 1) marked round r
     const uint8_t tag = (uint8_t)a.tag_cur;  // link_tag(r)
@@ -914,6 +944,7 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
         }
         block_add(newly, a.parts, r);
         if (a.work) block_add_u64(walked, a.work + (blockIdx.x & (kParts - 1)) * kWorkStride);
+        if constexpr (LM == 2 && HIN) tail_pack(a, *xp);
         return;
     }
     for (; v < end; v += step) newly += ps_actor<LM>(a, g, r, v, false);
