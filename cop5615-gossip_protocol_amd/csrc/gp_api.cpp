@@ -934,7 +934,8 @@ int launch_aux(Handle* h, int64_t k, const Xchg* x, int piece = 0) {
         // return at once: once the synced count has reached act_thr, every later round is such a round
         // (the count only grows), so the pass is not launched at all
         const bool tail = h->act[0] && h->act_thr && h->completed >= (int64_t)h->act_thr && k >= h->rounds + 1;
-        if (x && !tail) launch_ps_link_scatter_x(a, *x, l);
+        // (k_ps_quiet_x routes a dense round's link messages itself: kShardFuse)
+        if (x && !tail && !(kShardFuse && h->act[0])) launch_ps_link_scatter_x(a, *x, l);
         else if (!x && !fused_marks(h)) launch_link_count(a, l);
     }
     return GP_OK;

@@ -334,6 +334,12 @@ struct GsSparse {
                       // and the pack; 0 between launches)
 };
 constexpr uint32_t kSpStride = 32, kSpSlack = 1024;
+// A push-sum shard's dense round kernel (k_ps_quiet_x) routes its own link messages through LDS, and
+// k_ps_link_scatter_x is not launched (gp_kernels.hip, FuseStage).
+#ifndef GP_SHARD_FUSE
+#define GP_SHARD_FUSE 1
+#endif
+constexpr bool kShardFuse = GP_SHARD_FUSE != 0;
 // A push-sum shard's tail round counts its finished workgroups in kFinGroups groups (one counter per
 // 128-byte line) before one counter of groups (Xchg::fin).
 constexpr uint32_t kFinGroups = 32, kFinStride = 32;

@@ -204,6 +204,7 @@ struct PeerTab {
     uint32_t* slot[kMaxWorld];
     double2* msg[kMaxWorld];
     uint32_t cap[kMaxWorld];
+    uint32_t sbnd[kMaxWorld + 1];  // the ranks' slot bounds (owner_t: no SGPRs held for them in a walk)
 };
 __device__ __forceinline__ PeerTab& peer_tab() {
     __shared__ PeerTab t;
@@ -217,6 +218,14 @@ __device__ __forceinline__ void peer_tab_fill(const Xchg& x) {
         t.msg[threadIdx.x] = o.msg;
         t.cap[threadIdx.x] = o.cap;
     }
+    if (threadIdx.x <= x.world) peer_tab().sbnd[threadIdx.x] = x.sbnd[threadIdx.x];
+}
+// owner(x.sbnd, x.world, lp) from the LDS table (after peer_tab_fill and a barrier).
+__device__ __forceinline__ uint32_t owner_t(uint32_t world, uint32_t lp) {
+    const PeerTab& t = peer_tab();
+    uint32_t q = 0;
+    for (uint32_t i = 1; i < world; ++i) q += lp >= t.sbnd[i] ? 1u : 0u;
+    return q;
 }
 // The two halo faces' entry parts, likewise (a shard's tail round writes them itself).
 struct HaloTab {
@@ -270,6 +279,90 @@ __device__ __forceinline__ uint32_t wave_reserve(const Xchg& x, bool want, uint3
     if (want && (threadIdx.x & 63u) == lead) base = atomicAdd(ctr_at(x, q, my_sub()), (uint32_t)__popcll(mine));
     base = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead << 2), (int)base);
     return want ? base + mbcnt64(mine) : 0u;
+}
+
+// A shard's dense round routes its own link messages (kShardFuse): the round kernel has each message in
+// registers when its actor fires the extra link, so a remote one is staged in LDS (slot, message, peer,
+// position among the block's entries to that peer) instead of being re-read from msg_cur by a separate
+// pass over every actor (k_ps_link_scatter_x: 0.61 ms per C5 / 8 rank-round).  Every kFuseIters
+// iterations of the walk (block-uniform) the block reserves its staged entries' positions, one atomic
+// per peer, and writes the entries of the step before, whose reservation has come back meanwhile: two
+// stage buffers, so no workgroup waits for a returning atomic.  A step's entries go to sub-segment
+// (block + step) mod kSub, so a small grid still spreads them over every sub-segment.
+constexpr uint32_t kFuseStage = 256, kFuseIters = 4;
+struct FuseStage {
+    uint32_t n[2];                  // entries staged per buffer (past kFuseStage: placed directly)
+    uint32_t cnt[2][kMaxWorld];     // per peer
+    uint32_t base[kMaxWorld];       // the reserved positions of the buffer being written out
+    uint32_t slot[2][kFuseStage];
+    uint32_t qp[2][kFuseStage];     // peer << 16 | position among the buffer's entries to that peer
+    double2 msg[2][kFuseStage];
+};
+__device__ __forceinline__ FuseStage& fuse_stage() {
+    __shared__ FuseStage s;
+    return s;
+}
+// Walk state of the fused dense round (per thread, uniform over the block but res).
+struct FuseWalk {
+    uint32_t it = 0, step = 0, res = 0;  // res: thread q < world holds the last reservation of peer q
+};
+__device__ __forceinline__ uint32_t fuse_sub(uint32_t step) { return (blockIdx.x + step) % kSub; }
+// Before the block's first barrier.
+__device__ __forceinline__ void fuse_init() {
+    FuseStage& S = fuse_stage();
+    if (threadIdx.x < 2u) S.n[threadIdx.x] = 0u;
+    if (threadIdx.x < 2u * kMaxWorld) (&S.cnt[0][0])[threadIdx.x] = 0u;
+}
+// Stage one entry (any lane, divergent code).
+__device__ __forceinline__ void fuse_put(const Xchg& x, const FuseWalk& w, uint32_t q, uint32_t lp, double2 m) {
+    FuseStage& S = fuse_stage();
+    const uint32_t b = w.step & 1u;
+    const uint32_t i = atomicAdd(&S.n[b], 1u);
+    if (i < kFuseStage) {
+        const uint32_t p = atomicAdd(&S.cnt[b][q], 1u);
+        S.slot[b][i] = lp;
+        S.qp[b][i] = q << 16 | p;
+        S.msg[b][i] = m;
+    } else {  // the buffer is full (statistically never: 4 x 256 actors stage ~128): its own position
+        const uint32_t sub = fuse_sub(w.step);
+        put_t<true>(x, q, atomicAdd(ctr_at(x, q, sub), 1u), lp, m, sub);
+    }
+}
+// Write out buffer b (reserved at step s) with the bases in S.base.  Every thread calls it.
+__device__ __forceinline__ void fuse_write(const Xchg& x, uint32_t b, uint32_t n, uint32_t s) {
+    FuseStage& S = fuse_stage();
+    const uint32_t sub = fuse_sub(s);
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+        const uint32_t qp = S.qp[b][i], q = qp >> 16;
+        put_t<true>(x, q, S.base[q] + (qp & 0xFFFFu), S.slot[b][i], S.msg[b][i], sub);
+    }
+}
+// End of a step (block-uniform; every thread calls it): reserve this step's entries, write the previous
+// step's.  Returns whether any thread has actors left; when none has, also writes this step's (the end).
+__device__ __forceinline__ bool fuse_flush(const Xchg& x, FuseWalk& w, bool left) {
+    FuseStage& S = fuse_stage();
+    const bool more = __syncthreads_or(left);  // (the step's staging is done)
+    const uint32_t b = w.step & 1u, pb = b ^ 1u;
+    const uint32_t np = min(S.n[pb], kFuseStage), nb = min(S.n[b], kFuseStage);
+    if (threadIdx.x < x.world) {
+        S.base[threadIdx.x] = w.res;  // the previous step's reservation (issued one step ago)
+        const uint32_t c = S.cnt[b][threadIdx.x];
+        w.res = c ? atomicAdd(ctr_at(x, threadIdx.x, fuse_sub(w.step)), c) : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < kMaxWorld) S.cnt[pb][threadIdx.x] = 0u;
+    if (threadIdx.x == 0) S.n[pb] = 0u;
+    if (w.step) fuse_write(x, pb, np, w.step - 1u);
+    __syncthreads();  // (buffer pb and the bases are free again)
+    if (!more) {
+        if (threadIdx.x < x.world) S.base[threadIdx.x] = w.res;
+        __syncthreads();
+        fuse_write(x, b, nb, w.step);
+        return false;
+    }
+    w.step = (uint32_t)__builtin_amdgcn_readfirstlane((int)(w.step + 1u));
+    w.it = 0;
+    return true;
 }
 
 // ------------------------------------------------------------------ push-sum, grid topologies
@@ -543,6 +636,10 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                     lr[1] = r4.y;
                     lr[2] = r4.z;
                     lr[3] = r4.w;
+                    // (separate registers: a select over lanes of one vector value can become an indexed
+                    // read of a scratch copy when the kernel's registers are short, k_ps_quiet_x)
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; ++k) asm volatile("" : "+v"(lr[k]));
 #pragma unroll
                     for (uint32_t k = 0; k < 4; ++k) lc[k] = lr[k] & kRefTagMask;
                 } else {
@@ -569,7 +666,10 @@ __device__ __forceinline__ uint32_t ps_finish(const RoundArgs& a, const Geom& g,
                     if (LM == 2 && (u < a.olo || u >= a.ohi)) {
                         uint32_t rf = lr[0];
 #pragma unroll
-                        for (uint32_t q = 1; q < kLinkUnroll; ++q) rf = k == q ? lr[q] : rf;
+                        for (uint32_t q = 1; q < kLinkUnroll; ++q) {
+                            rf = k == q ? lr[q] : rf;
+                            asm volatile("" : "+v"(rf));  // (a select chain, not an indexed read)
+                        }
                         return a.rin_prev + (rf >> kRefShift);
                     }
                     return a.msg_prev + u;
@@ -879,10 +979,40 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
                 peer_tab_fill(*xp);
                 halo_tab_fill(*xp);
                 __syncthreads();
+            } else if constexpr (kShardFuse && !HIN) {  // a dense round stages its remote link messages
+                peer_tab_fill(*xp);
+                fuse_init();
+                __syncthreads();
+            }
+        }
+        uint32_t walked = 0;
+        if constexpr (LM == 2 && kShardFuse && !HIN) {
+            if (!tail) {  // a shard's dense round: its own walk, in block-uniform steps of kFuseIters
+                FuseWalk fw;
+                for (;;) {
+                    if (fw.it == kFuseIters && !fuse_flush(*xp, fw, v < end)) break;
+                    fw.it = (uint32_t)__builtin_amdgcn_readfirstlane((int)(fw.it + 1u));  // (uniform: an SGPR)
+                    const uint32_t u = v;
+                    v += step;
+                    if (u < end) {  // (a lane past its range walks nothing until the block's step ends)
+                        LinkSend ls;
+                        newly += ps_actor<LM, true, false>(a, g, r, u, mark, &ls);
+                        ++walked;
+                        if (ls.fired) {  // a local slot's mark, a remote one staged
+                            const Xchg& x = *xp;
+                            const uint32_t lp = a.lpos[u];
+                            const uint32_t q = owner_t(x.world, lp);
+                            if (q == x.rank) a.lref_cur[lp] = a.rtag_cur;
+                            else fuse_put(x, fw, q, lp, ls.msg);
+                        }
+                    }
+                }
+                block_add(newly, a.parts, r);
+                if (a.work) block_add_u64(walked, a.work + (blockIdx.x & (kParts - 1)) * kWorkStride);
+                return;
             }
         }
         TailWalk t = tail_walk(a, tail);
-        uint32_t walked = 0;
         for (;;) {
             uint32_t u;
             if (tail) {
@@ -968,11 +1098,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PSQ_W
 }
 // A shard of several ranks (LM 2): the same kernel with the exchange descriptor, so its tail rounds
 // route their own link messages (HIN: and write the halo faces).
+// <false> (dense rounds, and tail rounds the host cannot yet be sure of) also routes a dense round's
+// link messages through LDS (kShardFuse): a second walk loop, which needs more registers than seven
+// waves per SIMD leave (80 VGPRs and 106 SGPRs: six workgroups per CU, GP_PSQX_PER_CU).
+#ifndef GP_PSQX_PER_CU
+#define GP_PSQX_PER_CU (kShardFuse ? 6 : GP_PSQ_PER_CU)
+#endif
 template <bool HIN>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PSQ_WAVES))) GP_PSQ_SGPR_ATTR void k_ps_quiet_x(
+__global__ void k_ps_quiet_x(RoundArgs a, Xchg x);
+template <>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PSQ_WAVES))) GP_PSQ_SGPR_ATTR void k_ps_quiet_x<true>(
     RoundArgs a, Xchg x) {
-    ps_pull_body<2, true, HIN>(a, &x);
+    ps_pull_body<2, true, true>(a, &x);
 }
+#if GP_SHARD_FUSE
+template <>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) __attribute__((amdgpu_num_sgpr(106))) void
+k_ps_quiet_x<false>(RoundArgs a, Xchg x) {
+    ps_pull_body<2, true, false>(a, &x);
+}
+#else
+template <>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GP_PSQ_WAVES))) GP_PSQ_SGPR_ATTR void k_ps_quiet_x<false>(
+    RoundArgs a, Xchg x) {
+    ps_pull_body<2, true, false>(a, &x);
+}
+#endif
 
 
 // ------------------------------------------------------------------ small line grids: rounds in batches
@@ -3422,6 +3573,7 @@ uint32_t span_for(uint32_t n, int grid) {
 #define GP_PSQ_PER_CU 7
 #endif
 static int quiet_grid(const Launch& l) { return l.grid < 256 * GP_PSQ_PER_CU ? l.grid : 256 * GP_PSQ_PER_CU; }
+static int quiet_grid_x(const Launch& l) { return l.grid < 256 * GP_PSQX_PER_CU ? l.grid : 256 * GP_PSQX_PER_CU; }
 
 void launch_ps_tiny(const RoundArgs& a, int nk, hipStream_t s) {
     hipLaunchKernelGGL(k_ps_tiny, dim3(1), dim3(kTinyBlock), 0, s, a, (uint32_t)nk);
@@ -3456,7 +3608,7 @@ void launch_ps_pull(const RoundArgs& a, const Launch& l, const Xchg* x) {
         hipLaunchKernelGGL((k_ps_pull<3, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
     } else if (a.lref_prev) {  // a push-sum shard (slot references)
         if (q && x->hin) hipLaunchKernelGGL(k_ps_quiet_x<true>, dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a, *x);
-        else if (q) hipLaunchKernelGGL(k_ps_quiet_x<false>, dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a, *x);
+        else if (q) hipLaunchKernelGGL(k_ps_quiet_x<false>, dim3(quiet_grid_x(l)), dim3(kBlock), lds, l.stream, a, *x);
         else hipLaunchKernelGGL((k_ps_pull<2, false>), dim3(l.grid), dim3(kBlock), lds, l.stream, a);
     } else if (q) {
         hipLaunchKernelGGL((k_ps_quiet<1>), dim3(quiet_grid(l)), dim3(kBlock), lds, l.stream, a);
