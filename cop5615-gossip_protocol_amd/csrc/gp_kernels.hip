@@ -289,7 +289,10 @@ __device__ __forceinline__ uint32_t wave_reserve(const Xchg& x, bool want, uint3
 // per peer, and writes the entries of the step before, whose reservation has come back meanwhile: two
 // stage buffers, so no workgroup waits for a returning atomic.  A step's entries go to sub-segment
 // (block + step) mod kSub, so a small grid still spreads them over every sub-segment.
-constexpr uint32_t kFuseStage = 256, kFuseIters = 4;
+#ifndef GP_FUSE_STAGE
+#define GP_FUSE_STAGE 256  // (a test build with 8 sends most entries down the full-buffer path)
+#endif
+constexpr uint32_t kFuseStage = GP_FUSE_STAGE, kFuseIters = 4;
 struct FuseStage {
     uint32_t n[2];                  // entries staged per buffer (past kFuseStage: placed directly)
     uint32_t cnt[2][kMaxWorld];     // per peer
