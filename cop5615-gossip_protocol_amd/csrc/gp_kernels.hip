@@ -292,7 +292,10 @@ __device__ __forceinline__ uint32_t wave_reserve(const Xchg& x, bool want, uint3
 #ifndef GP_FUSE_STAGE
 #define GP_FUSE_STAGE 256  // (a test build with 8 sends most entries down the full-buffer path)
 #endif
-constexpr uint32_t kFuseStage = GP_FUSE_STAGE, kFuseIters = 4;
+#ifndef GP_FUSE_ITERS
+#define GP_FUSE_ITERS 4
+#endif
+constexpr uint32_t kFuseStage = GP_FUSE_STAGE, kFuseIters = GP_FUSE_ITERS;
 struct FuseStage {
     uint32_t n[2];                  // entries staged per buffer (past kFuseStage: placed directly)
     uint32_t cnt[2][kMaxWorld];     // per peer
