@@ -780,6 +780,7 @@ const char* aux_kernel_name(const Handle* h) {
     if (h->tiny) return "";
     if (h->generic) return h->gossip ? (h->sharded && h->world > 1 ? "k_shard_done_out" : "") : "k_scan_* + k_ps_push_fill";
     if (!h->g.has_link || fused_marks(h)) return "";
+    if (h->sharded && !h->gossip && kShardFuse && h->act[0]) return "";  // (routed by k_ps_quiet_x)
     if (h->sharded) return h->gossip ? "k_gs_link_scatter_x" : "k_ps_link_scatter_x";
     return "k_link_count";
 }
