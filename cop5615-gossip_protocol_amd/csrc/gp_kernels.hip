@@ -967,6 +967,14 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
         wave_add(newly, a.parts, r);
         return;
     }
+    // HIN (a round the host knows to be a tail round): the LDS tables filled and the walk's first marks
+    // in flight before the gate, whose barrier serves the tables too
+    TailWalk t0{};
+    if constexpr (LM == 2 && HIN) {
+        peer_tab_fill(*xp);
+        halo_tab_fill(*xp);
+        t0 = tail_walk(a, true);
+    }
     // converged after round r - 1 (one GPU, small graphs: Q = false, the per-wave gate)
     const unsigned long long prev = (Q || LM == 2) ? gate_count(a, a.r) : gate_count_wave(a, a.r);
     if (prev >= a.target) {  // (block-uniform; a tail round's headers still go out)
@@ -982,9 +990,11 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
             // a tail round's entries read the peers' chunks and the halo faces from LDS (put_t): a
             // lane's own peer or face indexing the kernel arguments is a vector load per field
             if (tail) {
-                peer_tab_fill(*xp);
-                halo_tab_fill(*xp);
-                __syncthreads();
+                if constexpr (!HIN) {
+                    peer_tab_fill(*xp);
+                    halo_tab_fill(*xp);
+                    __syncthreads();
+                }
             } else if constexpr (kShardFuse && !HIN) {  // a dense round stages its remote link messages
                 peer_tab_fill(*xp);
                 fuse_init();
@@ -1018,7 +1028,7 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
                 return;
             }
         }
-        TailWalk t = tail_walk(a, tail);
+        TailWalk t = HIN ? t0 : tail_walk(a, tail);
         for (;;) {
             uint32_t u;
             if (tail) {
