@@ -202,9 +202,10 @@ def _quiet_sweep_case(n, topo, world, seed, tight):
 
 
 def test_shards_quiet_default_and_work_count():
-    """Shards of 2^20 actors or more run the quiet kernel by default (k_ps_quiet_x), and count the
-    actors it walks in their timed rounds only, so work_per_launch averages over the same launches
-    as the kernel time: below the shard's actor count (the tail walks a few per cent of it)."""
+    """Shards of 2^20 actors or more run the quiet kernel by default (k_ps_quiet_x), which routes
+    every round's link messages itself (no k_ps_link_scatter_x: no aux kernel), and count the actors
+    it walks in their timed rounds only, so work_per_launch averages over the same launches as the
+    kernel time: below the shard's actor count (the tail walks a few per cent of it)."""
     n, world = 4_500_000, 2
     ref = Simulator(n, "Imp3D", "push-sum", seed=3)
     rs = ref.step()
@@ -215,6 +216,7 @@ def test_shards_quiet_default_and_work_count():
     for e in engines:
         ks = e.kernel_stats()
         assert ks["kernel"] == "k_ps_quiet_x", ks
+        assert ks["aux_kernel"] == "", ks  # (no link pass: the round kernel routes the links)
         assert ks["launches"] == (int(rs.round) + 7) // 8, ks  # every 8th round is timed
         assert 0 < ks["work_per_launch"] < e.hi - e.lo, ks
         e.close()
