@@ -1011,12 +1011,14 @@ __device__ __forceinline__ void ps_pull_body(const RoundArgs& a, const Xchg* xp 
                     const uint32_t u = v;
                     v += step;
                     if (u < end) {  // (a lane past its range walks nothing until the block's step ends)
+                        // the link's slot, loaded beside the actor's own loads (every line of lpos is
+                        // read anyway: one actor in seven fires its link)
+                        const uint32_t lp = a.lpos[u];
                         LinkSend ls;
                         newly += ps_actor<LM, true, false>(a, g, r, u, mark, &ls);
                         ++walked;
                         if (ls.fired) {  // a local slot's mark, a remote one staged
                             const Xchg& x = *xp;
-                            const uint32_t lp = a.lpos[u];
                             const uint32_t q = owner_t(x.world, lp);
                             if (q == x.rank) a.lref_cur[lp] = a.rtag_cur;
                             else fuse_put(x, fw, q, lp, ls.msg);
